@@ -1,0 +1,166 @@
+/*
+ * phgpu.h -- C-ABI of libphgpu.so, the MI355X (gfx950) progressive-hedging
+ * hot path.  Plain pointers and sizes only; every array argument marked
+ * "dev" is device memory owned by the caller (PyTorch-ROCm tensors in the
+ * Python host), every "host" array is read during the call only.
+ *
+ * Layout convention ("scenario-fastest"): a per-scenario vector v of length
+ * L over S scenarios is stored as v[i*S + s]  (i < L, s < S).
+ *
+ * Each entry point replaces one reference interface of mpi-sppy
+ * (/root/reference, Nov-2020 tree); citations are file:line there.
+ *
+ * Error model: every int-returning call returns 0 on success, or
+ *   PH_EINVAL (-1) invalid argument, PH_EHIP (-2) HIP runtime error,
+ *   PH_ENUM (-3) numerical failure.
+ * ph_last_error() returns a thread-local message for the last failure.
+ * Calls are stream-ordered on the stream given to ph_batch_create /
+ * ph_batch_set_stream and return without synchronising unless stated.
+ */
+#ifndef PHGPU_H
+#define PHGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PH_OK 0
+#define PH_EINVAL (-1)
+#define PH_EHIP (-2)
+#define PH_ENUM (-3)
+
+/* per-scenario solve status (phbase.py:959-989 maps 2/3 -> infeasible) */
+#define PH_STATUS_OPTIMAL 0
+#define PH_STATUS_ITERLIMIT 1
+#define PH_STATUS_PRIMAL_INFEASIBLE 2
+#define PH_STATUS_DUAL_INFEASIBLE 3
+
+typedef struct ph_batch *ph_batch_t;
+
+typedef struct ph_solve_opts {
+  double tol;          /* relative KKT tolerance (default 1e-9)            */
+  int32_t max_iters;   /* PDHG iteration cap per scenario (default 200000) */
+  int32_t check_every; /* KKT / restart check period (default 64)           */
+  int32_t warm_start;  /* 1: start from x,y,omega passed in (default 1)     */
+  double reflection;   /* Halpern reflection gamma in [0,1] (default 1.0)  */
+} ph_solve_opts;
+
+/* Library version string. */
+const char *ph_version(void);
+
+/* Thread-local message describing the last error. */
+const char *ph_last_error(void);
+
+/*
+ * Create a batch of S scenario subproblems sharing one sparsity pattern
+ *   min 1/2 x'diag(q)x + g'x  s.t.  rl <= A x <= ru,  l <= x <= u,
+ * A: m x n with nnz entries, CSR pattern (host arrays, int32).
+ * Replaces: per-scenario SolverFactory + set_instance
+ *   (mpisppy/phbase.py:1304-1362, _create_solvers).
+ * stream: a hipStream_t (may be NULL for the null stream).
+ */
+int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m,
+                    int32_t nnz, const int32_t *row_ptr /*host [m+1]*/,
+                    const int32_t *col_idx /*host [nnz]*/, void *stream);
+
+/* Change the stream later calls are ordered on. */
+int ph_batch_set_stream(ph_batch_t b, void *stream);
+
+/*
+ * Bind the per-scenario data (device, scenario-fastest) and compute the
+ * per-scenario Ruiz + Pock-Chambolle scaling and PDHG step size.  Must be
+ * called before ph_pdhg_solve; may be called again when data change.
+ * c is the objective in MIN form (negate for maximize models).
+ * The library copies what it needs; the caller may free the inputs after
+ * the stream has passed this call.
+ * Replaces: Pyomo model -> solver instance extraction (phbase.py:1327).
+ */
+int ph_batch_bind(ph_batch_t b, const double *vals /*dev [nnz][S]*/,
+                  const double *c /*dev [n][S]*/,
+                  const double *l /*dev [n][S]*/, const double *u /*dev [n][S]*/,
+                  const double *rl /*dev [m][S]*/, const double *ru /*dev [m][S]*/);
+
+/*
+ * Declare the K nonanticipative columns (same for every scenario):
+ * nonant_col[k] is the column of nonant slot k, in the reference's
+ * nonant order (scenario_tree.py:10-38, spbase.py:272-280).
+ */
+int ph_batch_set_nonants(ph_batch_t b, int32_t K,
+                         const int32_t *nonant_col /*host [K]*/);
+
+/*
+ * Batched PH subproblem solve (restarted, reflected-Halpern PDHG, FP64).
+ * The objective of scenario s is the reference's PH-augmented objective
+ * (phbase.py:1133-1209) in min form:
+ *   g = c + w_on*W - prox_on*rho*xbar   (nonant columns), q = prox_on*rho,
+ *   const = prox_on * sum_k rho_k/2 * xbar_k^2.
+ * W, rho, xbar: dev [K][S] (xbar already broadcast per scenario).
+ * x [n][S], y [m][S], omega [S] are read as the warm start when
+ * opts->warm_start and overwritten with the solution (unscaled).
+ * Outputs (dev [S]): status, iters, pobj (objective incl. const),
+ * dbound (dual objective incl. const = the scenario's outer bound).
+ * Replaces: solve_loop -> solve_one -> plugin.solve/load_vars/
+ *   results.Problem[0].Lower_bound (phbase.py:864-1095).
+ */
+int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho,
+                  const double *xbar, double w_on, double prox_on,
+                  double *x, double *y, double *omega, int32_t *status,
+                  int32_t *iters, double *pobj, double *dbound,
+                  const ph_solve_opts *opts);
+
+/*
+ * Per-node weighted sums for xbar / xsqbar (phbase.py:144-201, the local
+ * half of Compute_Xbar before the Allreduce).
+ * G "node slots": slot g covers nonant slot k = slot_k[g] for the scenarios
+ * s in [slot_s0[g], slot_s1[g]); out_sums[g] = sum prob_coeff[k][s]*x,
+ * out_sums[G+g] = sum prob_coeff[k][s]*x^2, x = x[nonant_col[k]][s].
+ * slot_k/slot_s0/slot_s1: dev int32 [G]; prob_coeff: dev [K][S];
+ * out_sums: dev [2G].
+ */
+int ph_xbar_accum(ph_batch_t b, const double *x, const double *prob_coeff,
+                  int32_t G, const int32_t *slot_k, const int32_t *slot_s0,
+                  const int32_t *slot_s1, double *out_sums);
+
+/*
+ * After the Allreduce of out_sums: broadcast xbar/xsqbar to every
+ * scenario, update W += rho*(x - xbar) (times w_coeff if not NULL) and
+ * return |x - xbar| summed over the nonants of each scenario.
+ * (phbase.py:204-217 broadcast, :224-251 Update_W, :266-272 conv local sum)
+ * gid: dev int32 [K][S] -> node slot g of (k,s); sums: dev [2G].
+ * xbar, xsqbar, W: dev [K][S] (out / out / in-out); absdiff: dev [S] (out).
+ * W may be NULL: broadcast and |x - xbar| sums only (Compute_Xbar alone).
+ */
+int ph_update_w(ph_batch_t b, const double *x, const double *sums, int32_t G,
+                const int32_t *gid, const double *rho, const double *w_coeff,
+                double *xbar, double *xsqbar, double *W, double *absdiff);
+
+/*
+ * Contiguous-segment sums: out[r] = sum_{s in [seg[r], seg[r+1])} v[s],
+ * r < R.  Used for convergence_diff's per-rank sums (phbase.py:266-276)
+ * and the probability-weighted Ebound/Eobjective partial sums.
+ * v: dev [S]; w: dev [S] weights or NULL; seg: dev int32 [R+1]; out: dev [R].
+ */
+int ph_segment_sum(ph_batch_t b, const double *v, const double *w, int32_t R,
+                   const int32_t *seg, double *out);
+
+/*
+ * Evaluate each scenario's active objective at x (phbase.py:279-312,
+ * Eobjective's per-scenario pyo.value(objfct)), min form incl. const.
+ * obj: dev [S].
+ */
+int ph_eval_objective(ph_batch_t b, const double *x, const double *W,
+                      const double *rho, const double *xbar, double w_on,
+                      double prox_on, double *obj);
+
+/* Block until all work queued on the batch's stream has finished. */
+int ph_batch_sync(ph_batch_t b);
+
+/* Free the handle and the library-owned device scratch. */
+void ph_batch_destroy(ph_batch_t b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHGPU_H */

@@ -1,0 +1,859 @@
+// phgpu.hip -- MI355X (gfx950) kernels + C-ABI for the batched PH hot path.
+//
+// Design:
+//  * one workgroup owns one scenario for a whole PDHG solve; the scenario's
+//    scaled matrix values, the current dual vector and the primal trial
+//    point live in LDS; every thread owns CPT columns and RPT rows whose
+//    state (x, anchor, objective, bounds, A x) lives in VGPRs;
+//  * one PDHG step = a column phase (SpMV^T through the CSC view of the
+//    shared pattern + primal prox step) and a row phase (SpMV through the
+//    CSR view + dual prox step), two workgroup barriers, no HBM traffic;
+//  * reflected Halpern iteration with adaptive restarts and primal-weight
+//    updates (r2HPDHG), KKT/restart checks every `check_every` steps with
+//    wave-shuffle + LDS block reductions;
+//  * the nonanticipativity kernels (xbar sums, W update, convergence sums)
+//    stream the scenario-fastest [k][s] arrays with coalesced FP64 loads.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/phgpu.h"
+
+#define PHGPU_VERSION "phgpu 0.1 gfx950"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_OK(expr)                                                        \
+  do {                                                                      \
+    hipError_t e_ = (expr);                                                 \
+    if (e_ != hipSuccess)                                                   \
+      return fail(PH_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int WAVE = 64;
+constexpr int MAX_WAVES = 16;  // 1024-thread blocks
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, WAVE);
+  return v;
+}
+
+// Block-wide sum of NV values.  `red` is LDS scratch of MAX_WAVES*NV doubles.
+// All threads receive the totals.  Contains two barriers.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double *red) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wid = threadIdx.x / WAVE;
+  const int nw = (blockDim.x + WAVE - 1) / WAVE;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double t = wave_sum(v[i]);
+    if (lane == 0) red[wid * NV + i] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += red[w * NV + i];
+    v[i] = t;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double clampd(double v, double lo, double hi) {
+  return fmin(fmax(v, lo), hi);
+}
+
+struct Pattern {
+  const int32_t *row_ptr;  // [m+1]
+  const int32_t *col_idx;  // [nnz]
+  const int32_t *col_ptr;  // [n+1]
+  const int32_t *csc_row;  // [nnz]
+  const int32_t *csc_k;    // [nnz]  CSR position of CSC entry
+};
+
+// ------------------------------------------------------------------------
+// Scaling kernel: per scenario Ruiz (10 sweeps) + Pock-Chambolle(alpha=1),
+// writes dr [S][m], dc [S][n], scaled values [S][nnz] and the step size
+// eta[s] = 0.995 / min(1, 1.02 * ||A~||_2 estimate) (||A~||_2 <= 1 after PC).
+// ------------------------------------------------------------------------
+template <int BLOCK, int CPT, int RPT>
+__global__ void __launch_bounds__(BLOCK) scale_kernel(
+    int S, int n, int m, int nnz, Pattern P, const double *__restrict__ vals,
+    double *__restrict__ vals_s, double *__restrict__ dr_out,
+    double *__restrict__ dc_out, double *__restrict__ eta_out) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int s = blockIdx.x;
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  double *av = lds;            // [nnz] working |values|
+  double *rsc = av + nnz;      // [m]
+  double *csc = rsc + m;       // [n]
+  double *vec = csc + n;       // [n] power iteration vector
+  double *wv = vec + n;        // [m]
+  double *red = wv + m;        // reduction scratch
+
+  for (int k = tid; k < nnz; k += T) av[k] = vals[(size_t)k * S + s];
+  for (int i = tid; i < m; i += T) rsc[i] = 1.0;
+  for (int j = tid; j < n; j += T) csc[j] = 1.0;
+  __syncthreads();
+
+  for (int sweep = 0; sweep < 11; ++sweep) {
+    const bool pc = (sweep == 10);  // last sweep: Pock-Chambolle (l1 norms)
+    // row factors
+    double rf[RPT];
+#pragma unroll
+    for (int b = 0; b < RPT; ++b) {
+      int i = tid + b * T;
+      rf[b] = 1.0;
+      if (i < m) {
+        double acc = 0.0;
+        for (int p = P.row_ptr[i]; p < P.row_ptr[i + 1]; ++p) {
+          double a = fabs(av[p]) * rsc[i] * csc[P.col_idx[p]];
+          acc = pc ? acc + a : fmax(acc, a);
+        }
+        rf[b] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
+      }
+    }
+    double cf[CPT];
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) {
+      int j = tid + b * T;
+      cf[b] = 1.0;
+      if (j < n) {
+        double acc = 0.0;
+        for (int p = P.col_ptr[j]; p < P.col_ptr[j + 1]; ++p) {
+          int i = P.csc_row[p];
+          double a = fabs(av[P.csc_k[p]]) * rsc[i] * csc[j];
+          acc = pc ? acc + a : fmax(acc, a);
+        }
+        cf[b] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < RPT; ++b) {
+      int i = tid + b * T;
+      if (i < m) rsc[i] *= rf[b];
+    }
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) {
+      int j = tid + b * T;
+      if (j < n) csc[j] *= cf[b];
+    }
+    __syncthreads();
+  }
+  // scaled values
+  for (int i = tid; i < m; i += T) {
+    for (int p = P.row_ptr[i]; p < P.row_ptr[i + 1]; ++p)
+      av[p] = av[p] * rsc[i] * csc[P.col_idx[p]];
+  }
+  for (int j = tid; j < n; j += T) vec[j] = 1.0;
+  __syncthreads();
+  // power iteration on A~^T A~
+  double est = 1.0;
+  for (int it = 0; it < 64; ++it) {
+    for (int i = tid; i < m; i += T) {
+      double acc = 0.0;
+      for (int p = P.row_ptr[i]; p < P.row_ptr[i + 1]; ++p) acc += av[p] * vec[P.col_idx[p]];
+      wv[i] = acc;
+    }
+    __syncthreads();
+    double nv[1] = {0.0};
+    double tv[CPT];
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) {
+      int j = tid + b * T;
+      tv[b] = 0.0;
+      if (j < n) {
+        double acc = 0.0;
+        for (int p = P.col_ptr[j]; p < P.col_ptr[j + 1]; ++p) acc += av[P.csc_k[p]] * wv[P.csc_row[p]];
+        tv[b] = acc;
+        nv[0] += acc * acc;
+      }
+    }
+    block_sum<1>(nv, red);
+    double nrm = sqrt(nv[0]);
+    est = sqrt(nrm);  // ||A^T A v|| with ||v||=1 -> sigma_max^2 estimate
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) {
+      int j = tid + b * T;
+      if (j < n) vec[j] = nrm > 0.0 ? tv[b] / nrm : 0.0;
+    }
+    __syncthreads();
+  }
+  for (int k = tid; k < nnz; k += T) vals_s[(size_t)s * nnz + k] = av[k];
+  for (int i = tid; i < m; i += T) dr_out[(size_t)s * m + i] = rsc[i];
+  for (int j = tid; j < n; j += T) dc_out[(size_t)s * n + j] = csc[j];
+  if (tid == 0) {
+    double sn = fmin(1.0, 1.02 * est);
+    if (!(sn > 1e-12)) sn = 1.0;
+    eta_out[s] = 0.995 / sn;
+  }
+}
+
+struct SolveArgs {
+  int S, n, m, nnz;
+  Pattern P;
+  const double *vals_s, *dr, *dc, *eta;
+  const double *c, *l, *u, *rl, *ru;
+  const int32_t *slot_of_col;
+  const double *W, *rho, *xbar;
+  double w_on, prox_on;
+  double *x, *y, *omega;
+  int32_t *status, *iters;
+  double *pobj, *dbound;
+  double tol;
+  int max_iters, check_every, warm;
+  double refl;
+};
+
+// ------------------------------------------------------------------------
+// PDHG solve kernel: one workgroup per scenario, everything on chip.
+// ------------------------------------------------------------------------
+template <int BLOCK, int CPT, int RPT>
+__global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int s = blockIdx.x;
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  const int S = a.S, n = a.n, m = a.m, nnz = a.nnz;
+  double *vals = lds;         // [nnz] scaled A~
+  double *xs = vals + nnz;    // [n]   primal trial point x^+ (shared)
+  double *ys = xs + n;        // [m]   dual iterate / dual trial (shared)
+  double *red = ys + m;       // reduction scratch [MAX_WAVES*8]
+
+  const double *vs = a.vals_s + (size_t)s * nnz;
+  for (int k = tid; k < nnz; k += T) vals[k] = vs[k];
+
+  // ---- column state in registers
+  double X[CPT], Z0X[CPT], G[CPT], Q[CPT], L[CPT], U[CPT], DC[CPT], XN[CPT];
+  double cst = 0.0, gsq = 0.0;
+#pragma unroll
+  for (int b = 0; b < CPT; ++b) {
+    int j = tid + b * T;
+    X[b] = Z0X[b] = G[b] = Q[b] = XN[b] = 0.0;
+    L[b] = U[b] = 0.0;
+    DC[b] = 1.0;
+    if (j < n) {
+      double dcj = a.dc[(size_t)s * n + j];
+      double g = a.c[(size_t)j * S + s], q = 0.0;
+      int k = a.slot_of_col ? a.slot_of_col[j] : -1;
+      if (k >= 0) {
+        double W = a.W[(size_t)k * S + s], r = a.rho[(size_t)k * S + s];
+        double xb = a.xbar[(size_t)k * S + s];
+        g += a.w_on * W - a.prox_on * r * xb;
+        q = a.prox_on * r;
+        cst += a.prox_on * 0.5 * r * xb * xb;
+      }
+      DC[b] = dcj;
+      G[b] = g * dcj;
+      Q[b] = q * dcj * dcj;
+      L[b] = a.l[(size_t)j * S + s] / dcj;
+      U[b] = a.u[(size_t)j * S + s] / dcj;
+      double x0 = a.warm ? a.x[(size_t)j * S + s] / dcj : 0.0;
+      X[b] = clampd(x0, L[b], U[b]);
+      Z0X[b] = X[b];
+      gsq += G[b] * G[b];
+    }
+  }
+  // ---- row state in registers
+  double Y[RPT], Z0Y[RPT], AX[RPT], AZ0[RPT], RL[RPT], RU[RPT], DR[RPT];
+  double YN[RPT], AXN[RPT];
+  double bsq = 0.0;
+#pragma unroll
+  for (int b = 0; b < RPT; ++b) {
+    int i = tid + b * T;
+    Y[b] = Z0Y[b] = AX[b] = AZ0[b] = RL[b] = RU[b] = YN[b] = AXN[b] = 0.0;
+    DR[b] = 1.0;
+    if (i < m) {
+      double d = a.dr[(size_t)s * m + i];
+      DR[b] = d;
+      RL[b] = a.rl[(size_t)i * S + s] * d;
+      RU[b] = a.ru[(size_t)i * S + s] * d;
+      Y[b] = a.warm ? a.y[(size_t)i * S + s] / d : 0.0;
+      // keep the dual iterate sign-feasible for the row's bounds
+      if (!isfinite(RL[b])) Y[b] = fmin(Y[b], 0.0);
+      if (!isfinite(RU[b])) Y[b] = fmax(Y[b], 0.0);
+      Z0Y[b] = Y[b];
+      double bl = isfinite(RL[b]) ? RL[b] : 0.0;
+      double bu = isfinite(RU[b]) ? RU[b] : 0.0;
+      bsq += bl * bl + (isfinite(RL[b]) ? 0.0 : bu * bu);
+    }
+  }
+  // initial primal weight, objective constant
+  double omega;
+  {
+    double v[3] = {cst, gsq, bsq};
+    block_sum<3>(v, red);
+    cst = v[0];
+    double gn = sqrt(v[1]), bn = sqrt(v[2]);
+    omega = (gn > 1e-10 && bn > 1e-10) ? gn / bn : 1.0;
+    if (a.warm && a.omega[s] > 0.0) omega = a.omega[s];
+  }
+  const double eta = a.eta[s];
+  const double gam = a.refl;
+
+  // A x for the starting point; ys <- y
+#pragma unroll
+  for (int b = 0; b < CPT; ++b) {
+    int j = tid + b * T;
+    if (j < n) xs[j] = X[b];
+  }
+#pragma unroll
+  for (int b = 0; b < RPT; ++b) {
+    int i = tid + b * T;
+    if (i < m) ys[i] = Y[b];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < RPT; ++b) {
+    int i = tid + b * T;
+    if (i < m) {
+      double acc = 0.0;
+      for (int p = a.P.row_ptr[i]; p < a.P.row_ptr[i + 1]; ++p) acc += vals[p] * xs[a.P.col_idx[p]];
+      AX[b] = AZ0[b] = acc;
+    }
+  }
+  __syncthreads();
+
+  int k = 0;  // iterations since last restart
+  int it = 0;
+  int stat = PH_STATUS_ITERLIMIT;
+  double r_restart = -1.0, r_prev = -1.0;
+  double out_pobj = 0.0, out_dobj = 0.0;
+  const int maxit = a.max_iters;
+  const int chk = a.check_every > 0 ? a.check_every : 64;
+
+  for (it = 0; it < maxit; ++it) {
+    const double tau = eta / omega, sig = eta * omega;
+    const double ca = (double)(k + 1) / (double)(k + 2);
+    const double cb = 1.0 / (double)(k + 2);
+    const bool check = (it % chk) == 0 || it == maxit - 1;
+    double dxx = 0.0, dyy = 0.0;
+
+    // ---- column phase: x+ = clip((x - tau(g - A^T y)) / (1 + tau q))
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) {
+      int j = tid + b * T;
+      if (j < n) {
+        double aty = 0.0;
+        for (int p = a.P.col_ptr[j]; p < a.P.col_ptr[j + 1]; ++p)
+          aty += vals[a.P.csc_k[p]] * ys[a.P.csc_row[p]];
+        double xn = clampd((X[b] - tau * (G[b] - aty)) / (1.0 + tau * Q[b]), L[b], U[b]);
+        double d = xn - X[b];
+        dxx += d * d;
+        XN[b] = xn;
+        X[b] = ca * ((1.0 + gam) * xn - gam * X[b]) + cb * Z0X[b];
+        xs[j] = xn;
+      }
+    }
+    __syncthreads();
+    // ---- row phase: y+ = prox(y - sig A(2x+ - x))
+#pragma unroll
+    for (int b = 0; b < RPT; ++b) {
+      int i = tid + b * T;
+      if (i < m) {
+        double axn = 0.0;
+        for (int p = a.P.row_ptr[i]; p < a.P.row_ptr[i + 1]; ++p)
+          axn += vals[p] * xs[a.P.col_idx[p]];
+        double v = Y[b] - sig * (2.0 * axn - AX[b]);
+        double yn = fmax(v + sig * RL[b], 0.0) + fmin(v + sig * RU[b], 0.0);
+        double d = yn - Y[b];
+        dyy += d * d;
+        YN[b] = yn;
+        AXN[b] = axn;
+        Y[b] = ca * ((1.0 + gam) * yn - gam * Y[b]) + cb * Z0Y[b];
+        AX[b] = ca * ((1.0 + gam) * axn - gam * AX[b]) + cb * AZ0[b];
+      }
+    }
+    ++k;
+    if (!check) {
+#pragma unroll
+      for (int b = 0; b < RPT; ++b) {
+        int i = tid + b * T;
+        if (i < m) ys[i] = Y[b];
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- check: KKT of the trial point (x+, y+) in the unscaled space
+    __syncthreads();  // every thread done reading xs in the row phase
+#pragma unroll
+    for (int b = 0; b < RPT; ++b) {
+      int i = tid + b * T;
+      if (i < m) ys[i] = YN[b];
+    }
+    __syncthreads();
+    double pr2 = 0.0, dr2 = 0.0, po = 0.0, dob = 0.0, ddx = 0.0, ddy = 0.0, bl2 = 0.0, g2 = 0.0;
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) {
+      int j = tid + b * T;
+      if (j < n) {
+        double aty = 0.0;
+        for (int p = a.P.col_ptr[j]; p < a.P.col_ptr[j + 1]; ++p)
+          aty += vals[a.P.csc_k[p]] * ys[a.P.csc_row[p]];
+        double lam = (Q[b] * XN[b] + G[b] - aty) / DC[b];  // unscaled reduced cost
+        double xu = XN[b] * DC[b];
+        double lu = L[b] * DC[b], uu = U[b] * DC[b];
+        double lp = isfinite(lu) ? fmax(lam, 0.0) : 0.0;
+        double lm = isfinite(uu) ? fmin(lam, 0.0) : 0.0;
+        double rd = lam - lp - lm;
+        dr2 += rd * rd;
+        double qx = Q[b] / (DC[b] * DC[b]);
+        double gu = G[b] / DC[b];
+        po += 0.5 * qx * xu * xu + gu * xu;
+        dob += -0.5 * qx * xu * xu + (lp > 0.0 ? lp * lu : 0.0) + (lm < 0.0 ? lm * uu : 0.0);
+        g2 += gu * gu;
+        double e = XN[b] - Z0X[b];
+        ddx += e * e;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < RPT; ++b) {
+      int i = tid + b * T;
+      if (i < m) {
+        double axu = AXN[b] / DR[b];
+        double rlu = RL[b] / DR[b], ruu = RU[b] / DR[b];
+        double rp = axu - clampd(axu, rlu, ruu);
+        pr2 += rp * rp;
+        double yu = YN[b] * DR[b];
+        dob += (yu > 0.0 ? yu * rlu : 0.0) + (yu < 0.0 ? yu * ruu : 0.0);
+        if (isfinite(rlu)) bl2 += rlu * rlu;
+        double e = YN[b] - Z0Y[b];
+        ddy += e * e;
+      }
+    }
+    double v[10] = {pr2, dr2, po, dob, ddx, ddy, bl2, g2, dxx, dyy};
+    block_sum<10>(v, red);
+    const double ep = sqrt(v[0]) / (1.0 + sqrt(v[6]));
+    const double ed = sqrt(v[1]) / (1.0 + sqrt(v[7]));
+    const double P0 = v[2] + cst, D0 = v[3] + cst;
+    const double eg = fabs(P0 - D0) / (1.0 + fabs(P0) + fabs(D0));
+    out_pobj = P0;
+    out_dobj = D0;
+    const double r = sqrt(omega * v[8] + v[9] / omega);
+    if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
+      stat = PH_STATUS_OPTIMAL;
+#pragma unroll
+      for (int b = 0; b < CPT; ++b) X[b] = XN[b];
+#pragma unroll
+      for (int b = 0; b < RPT; ++b) Y[b] = YN[b];
+      ++it;
+      break;
+    }
+    bool restart = false;
+    if (r_restart < 0.0) {
+      r_restart = r;
+    } else {
+      restart = (r <= 0.2 * r_restart) || (r <= 0.8 * r_restart && r > r_prev) ||
+                (k >= 0.36 * (double)(it + 1));
+    }
+    r_prev = r;
+    if (restart) {
+      const double dx = sqrt(v[4]), dy = sqrt(v[5]);
+      if (dx > 1e-12 && dy > 1e-12) omega = exp(0.5 * log(dy / dx) + 0.5 * log(omega));
+#pragma unroll
+      for (int b = 0; b < CPT; ++b) X[b] = Z0X[b] = XN[b];
+#pragma unroll
+      for (int b = 0; b < RPT; ++b) {
+        Y[b] = Z0Y[b] = YN[b];
+        AX[b] = AZ0[b] = AXN[b];
+      }
+      k = 0;
+      r_restart = r;
+    }
+    __syncthreads();  // all reads of ys (check col phase) done
+#pragma unroll
+    for (int b = 0; b < RPT; ++b) {
+      int i = tid + b * T;
+      if (i < m) ys[i] = Y[b];
+    }
+    __syncthreads();
+  }
+
+  // ---- write back (unscaled, scenario-fastest)
+#pragma unroll
+  for (int b = 0; b < CPT; ++b) {
+    int j = tid + b * T;
+    if (j < n) a.x[(size_t)j * S + s] = X[b] * DC[b];
+  }
+#pragma unroll
+  for (int b = 0; b < RPT; ++b) {
+    int i = tid + b * T;
+    if (i < m) a.y[(size_t)i * S + s] = Y[b] * DR[b];
+  }
+  if (tid == 0) {
+    a.omega[s] = omega;
+    a.status[s] = stat;
+    a.iters[s] = it;
+    a.pobj[s] = out_pobj;
+    a.dbound[s] = out_dobj;
+  }
+}
+
+// ------------------------------------------------------------------------
+// nonanticipativity kernels (scenario-fastest, coalesced)
+// ------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) xbar_accum_kernel(
+    int S, const double *__restrict__ x, const double *__restrict__ pc,
+    const int32_t *__restrict__ nonant_col, const int32_t *__restrict__ slot_k,
+    const int32_t *__restrict__ s0, const int32_t *__restrict__ s1, int G,
+    double *__restrict__ out) {
+  __shared__ double red[MAX_WAVES * 2];
+  const int g = blockIdx.x;
+  const int k = slot_k[g];
+  const double *xr = x + (size_t)nonant_col[k] * S;
+  const double *pr = pc + (size_t)k * S;
+  double v[2] = {0.0, 0.0};
+  for (int s = s0[g] + threadIdx.x; s < s1[g]; s += blockDim.x) {
+    double xv = xr[s], p = pr[s];
+    v[0] += p * xv;
+    v[1] += p * xv * xv;
+  }
+  block_sum<2>(v, red);
+  if (threadIdx.x == 0) {
+    out[g] = v[0];
+    out[G + g] = v[1];
+  }
+}
+
+__global__ void __launch_bounds__(256) update_w_kernel(
+    int S, int K, const double *__restrict__ x, const int32_t *__restrict__ nonant_col,
+    const double *__restrict__ sums, int G, const int32_t *__restrict__ gid,
+    const double *__restrict__ rho, const double *__restrict__ wc,
+    double *__restrict__ xbar, double *__restrict__ xsqbar, double *__restrict__ W,
+    double *__restrict__ absdiff) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  double acc = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const size_t o = (size_t)k * S + s;
+    const int g = gid[o];
+    const double xb = sums[g], xsq = sums[G + g];
+    const double xv = x[(size_t)nonant_col[k] * S + s];
+    xbar[o] = xb;
+    xsqbar[o] = xsq;
+    const double d = xv - xb;
+    if (W) {
+      double w = W[o] + rho[o] * d;
+      if (wc) w *= wc[o];
+      W[o] = w;
+    }
+    acc += fabs(d);
+  }
+  absdiff[s] = acc;
+}
+
+__global__ void __launch_bounds__(256) segment_sum_kernel(
+    const double *__restrict__ v, const double *__restrict__ w,
+    const int32_t *__restrict__ seg, double *__restrict__ out) {
+  __shared__ double red[MAX_WAVES];
+  const int r = blockIdx.x;
+  double acc[1] = {0.0};
+  for (int s = seg[r] + threadIdx.x; s < seg[r + 1]; s += blockDim.x)
+    acc[0] += w ? w[s] * v[s] : v[s];
+  block_sum<1>(acc, red);
+  if (threadIdx.x == 0) out[r] = acc[0];
+}
+
+__global__ void __launch_bounds__(256) eval_obj_kernel(
+    int S, int n, const double *__restrict__ c, const int32_t *__restrict__ slot_of_col,
+    const double *__restrict__ x, const double *__restrict__ W,
+    const double *__restrict__ rho, const double *__restrict__ xbar, double w_on,
+    double prox_on, double *__restrict__ obj) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  double acc = 0.0;
+  for (int j = 0; j < n; ++j) {
+    const double xv = x[(size_t)j * S + s];
+    acc += c[(size_t)j * S + s] * xv;
+    const int k = slot_of_col[j];
+    if (k >= 0) {
+      const size_t o = (size_t)k * S + s;
+      const double xb = xbar[o], r = rho[o];
+      acc += w_on * W[o] * xv + prox_on * 0.5 * r * (xv * xv - 2.0 * xb * xv + xb * xb);
+    }
+  }
+  obj[s] = acc;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------
+// handle
+// --------------------------------------------------------------------------
+struct ph_batch {
+  int S = 0, n = 0, m = 0, nnz = 0, K = 0;
+  hipStream_t stream = nullptr;
+  int32_t *d_row_ptr = nullptr, *d_col_idx = nullptr, *d_col_ptr = nullptr;
+  int32_t *d_csc_row = nullptr, *d_csc_k = nullptr;
+  int32_t *d_slot_of_col = nullptr, *d_nonant_col = nullptr;
+  double *d_vals_s = nullptr, *d_dr = nullptr, *d_dc = nullptr, *d_eta = nullptr;
+  double *d_c = nullptr, *d_l = nullptr, *d_u = nullptr, *d_rl = nullptr, *d_ru = nullptr;
+  bool bound = false;
+  int per = 1, block = 64;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(T **p, size_t count) {
+  if (count == 0) count = 1;
+  HIP_OK(hipMalloc((void **)p, count * sizeof(T)));
+  return 0;
+}
+
+// Block size and columns/rows per thread.  Per-thread register state is
+// ~17 doubles per slot, so slots per thread stay <= 6 (VGPR budget at two
+// waves per SIMD); larger scenarios need the streaming kernel (not built).
+bool pick_geometry(int n, int m, int *block, int *per) {
+  const int mx = n > m ? n : m;
+  if (mx <= 64) { *block = 64; *per = 1; }
+  else if (mx <= 128) { *block = 128; *per = 1; }
+  else if (mx <= 256) { *block = 256; *per = 1; }
+  else if (mx <= 512) { *block = 256; *per = 2; }
+  else if (mx <= 1024) { *block = 512; *per = 2; }
+  else if (mx <= 1536) { *block = 512; *per = 3; }
+  else if (mx <= 2048) { *block = 512; *per = 4; }
+  else if (mx <= 3072) { *block = 512; *per = 6; }
+  else return false;
+  return true;
+}
+
+#define DISPATCH_GEOM(BLK, PER, ...)                                            \
+  do {                                                                          \
+    if (BLK == 64 && PER == 1) { constexpr int B_ = 64, P_ = 1; __VA_ARGS__; }   \
+    else if (BLK == 128 && PER == 1) { constexpr int B_ = 128, P_ = 1; __VA_ARGS__; } \
+    else if (BLK == 256 && PER == 1) { constexpr int B_ = 256, P_ = 1; __VA_ARGS__; } \
+    else if (BLK == 256 && PER == 2) { constexpr int B_ = 256, P_ = 2; __VA_ARGS__; } \
+    else if (BLK == 512 && PER == 2) { constexpr int B_ = 512, P_ = 2; __VA_ARGS__; } \
+    else if (BLK == 512 && PER == 3) { constexpr int B_ = 512, P_ = 3; __VA_ARGS__; } \
+    else if (BLK == 512 && PER == 4) { constexpr int B_ = 512, P_ = 4; __VA_ARGS__; } \
+    else if (BLK == 512 && PER == 6) { constexpr int B_ = 512, P_ = 6; __VA_ARGS__; } \
+    else return fail(PH_EINVAL, "internal: no kernel instance for this geometry"); \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+const char *ph_version(void) { return PHGPU_VERSION; }
+
+const char *ph_last_error(void) { return g_err.c_str(); }
+
+int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nnz,
+                    const int32_t *row_ptr, const int32_t *col_idx, void *stream) {
+  if (!out || S <= 0 || n <= 0 || m < 0 || nnz < 0 || !row_ptr || (nnz > 0 && !col_idx))
+    return fail(PH_EINVAL, "ph_batch_create: bad arguments");
+  if (row_ptr[0] != 0 || row_ptr[m] != nnz) return fail(PH_EINVAL, "ph_batch_create: row_ptr inconsistent with nnz");
+  for (int i = 0; i < m; ++i)
+    if (row_ptr[i + 1] < row_ptr[i]) return fail(PH_EINVAL, "ph_batch_create: row_ptr not monotone");
+  for (int p = 0; p < nnz; ++p)
+    if (col_idx[p] < 0 || col_idx[p] >= n) return fail(PH_EINVAL, "ph_batch_create: col_idx out of range");
+  // CSC view of the shared pattern
+  std::vector<int32_t> col_ptr(n + 1, 0), csc_row(nnz), csc_k(nnz);
+  for (int p = 0; p < nnz; ++p) col_ptr[col_idx[p] + 1]++;
+  for (int j = 0; j < n; ++j) col_ptr[j + 1] += col_ptr[j];
+  std::vector<int32_t> fill(col_ptr.begin(), col_ptr.end() - 1);
+  for (int i = 0; i < m; ++i)
+    for (int p = row_ptr[i]; p < row_ptr[i + 1]; ++p) {
+      int q = fill[col_idx[p]]++;
+      csc_row[q] = i;
+      csc_k[q] = p;
+    }
+  ph_batch *b = new ph_batch();
+  b->S = S; b->n = n; b->m = m; b->nnz = nnz;
+  b->stream = (hipStream_t)stream;
+  if (!pick_geometry(n, m, &b->block, &b->per))
+    return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns; the on-chip PDHG kernel does not cover it");
+  int rc = 0;
+  if ((rc = dalloc(&b->d_row_ptr, m + 1)) || (rc = dalloc(&b->d_col_idx, nnz)) ||
+      (rc = dalloc(&b->d_col_ptr, n + 1)) || (rc = dalloc(&b->d_csc_row, nnz)) ||
+      (rc = dalloc(&b->d_csc_k, nnz)) || (rc = dalloc(&b->d_slot_of_col, n)) ||
+      (rc = dalloc(&b->d_vals_s, (size_t)S * nnz)) || (rc = dalloc(&b->d_dr, (size_t)S * m)) ||
+      (rc = dalloc(&b->d_dc, (size_t)S * n)) || (rc = dalloc(&b->d_eta, S)) ||
+      (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
+      (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
+      (rc = dalloc(&b->d_ru, (size_t)S * m))) {
+    ph_batch_destroy(b);
+    return rc;
+  }
+  std::vector<int32_t> noslot(n, -1);
+  auto cp = [&](void *d, const void *h, size_t bytes) {
+    return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, b->stream);
+  };
+  if (cp(b->d_row_ptr, row_ptr, sizeof(int32_t) * (m + 1)) != hipSuccess ||
+      (nnz && cp(b->d_col_idx, col_idx, sizeof(int32_t) * nnz) != hipSuccess) ||
+      cp(b->d_col_ptr, col_ptr.data(), sizeof(int32_t) * (n + 1)) != hipSuccess ||
+      (nnz && cp(b->d_csc_row, csc_row.data(), sizeof(int32_t) * nnz) != hipSuccess) ||
+      (nnz && cp(b->d_csc_k, csc_k.data(), sizeof(int32_t) * nnz) != hipSuccess) ||
+      cp(b->d_slot_of_col, noslot.data(), sizeof(int32_t) * n) != hipSuccess ||
+      hipStreamSynchronize(b->stream) != hipSuccess) {
+    ph_batch_destroy(b);
+    return fail(PH_EHIP, "ph_batch_create: copying the pattern failed");
+  }
+  *out = b;
+  return PH_OK;
+}
+
+int ph_batch_set_stream(ph_batch_t b, void *stream) {
+  if (!b) return fail(PH_EINVAL, "null batch");
+  b->stream = (hipStream_t)stream;
+  return PH_OK;
+}
+
+static size_t scale_lds_bytes(const ph_batch *b) {
+  return sizeof(double) * ((size_t)b->nnz + 2 * b->m + 2 * b->n + MAX_WAVES * 8);
+}
+static size_t solve_lds_bytes(const ph_batch *b) {
+  return sizeof(double) * ((size_t)b->nnz + b->n + b->m + MAX_WAVES * 10);
+}
+
+int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const double *l,
+                  const double *u, const double *rl, const double *ru) {
+  if (!b || (!vals && b->nnz) || !c || !l || !u || (b->m && (!rl || !ru)))
+    return fail(PH_EINVAL, "ph_batch_bind: null argument");
+  const size_t Sn = (size_t)b->S * b->n, Sm = (size_t)b->S * b->m;
+  HIP_OK(hipMemcpyAsync(b->d_c, c, Sn * 8, hipMemcpyDeviceToDevice, b->stream));
+  HIP_OK(hipMemcpyAsync(b->d_l, l, Sn * 8, hipMemcpyDeviceToDevice, b->stream));
+  HIP_OK(hipMemcpyAsync(b->d_u, u, Sn * 8, hipMemcpyDeviceToDevice, b->stream));
+  if (Sm) {
+    HIP_OK(hipMemcpyAsync(b->d_rl, rl, Sm * 8, hipMemcpyDeviceToDevice, b->stream));
+    HIP_OK(hipMemcpyAsync(b->d_ru, ru, Sm * 8, hipMemcpyDeviceToDevice, b->stream));
+  }
+  const size_t lds = scale_lds_bytes(b);
+  if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_batch_bind: scenario does not fit in LDS (nnz+2n+2m too large)");
+  Pattern P{b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k};
+  DISPATCH_GEOM(b->block, b->per, {
+    hipLaunchKernelGGL((scale_kernel<B_, P_, P_>), dim3(b->S), dim3(B_), lds, b->stream,
+                       b->S, b->n, b->m, b->nnz, P, vals, b->d_vals_s, b->d_dr, b->d_dc, b->d_eta);
+  });
+  HIP_OK(hipGetLastError());
+  b->bound = true;
+  return PH_OK;
+}
+
+int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
+  if (!b || K < 0 || (K && !nonant_col)) return fail(PH_EINVAL, "ph_batch_set_nonants: bad arguments");
+  std::vector<int32_t> slot(b->n, -1);
+  for (int k = 0; k < K; ++k) {
+    if (nonant_col[k] < 0 || nonant_col[k] >= b->n) return fail(PH_EINVAL, "nonant column out of range");
+    if (slot[nonant_col[k]] >= 0) return fail(PH_EINVAL, "nonant column listed twice");
+    slot[nonant_col[k]] = k;
+  }
+  if (b->d_nonant_col) (void)hipFree(b->d_nonant_col);
+  b->d_nonant_col = nullptr;
+  int rc = dalloc(&b->d_nonant_col, K);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(b->d_nonant_col, nonant_col, sizeof(int32_t) * (K ? K : 0), hipMemcpyHostToDevice, b->stream));
+  HIP_OK(hipMemcpyAsync(b->d_slot_of_col, slot.data(), sizeof(int32_t) * b->n, hipMemcpyHostToDevice, b->stream));
+  HIP_OK(hipStreamSynchronize(b->stream));
+  b->K = K;
+  return PH_OK;
+}
+
+int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double *xbar,
+                  double w_on, double prox_on, double *x, double *y, double *omega,
+                  int32_t *status, int32_t *iters, double *pobj, double *dbound,
+                  const ph_solve_opts *opts) {
+  if (!b || !b->bound) return fail(PH_EINVAL, "ph_pdhg_solve: batch not bound");
+  if (!x || (b->m && !y) || !omega || !status || !iters || !pobj || !dbound)
+    return fail(PH_EINVAL, "ph_pdhg_solve: null output");
+  if (b->K && (!W || !rho || !xbar)) return fail(PH_EINVAL, "ph_pdhg_solve: null W/rho/xbar");
+  SolveArgs a;
+  a.S = b->S; a.n = b->n; a.m = b->m; a.nnz = b->nnz;
+  a.P = Pattern{b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k};
+  a.vals_s = b->d_vals_s; a.dr = b->d_dr; a.dc = b->d_dc; a.eta = b->d_eta;
+  a.c = b->d_c; a.l = b->d_l; a.u = b->d_u; a.rl = b->d_rl; a.ru = b->d_ru;
+  a.slot_of_col = b->d_slot_of_col;
+  a.W = W; a.rho = rho; a.xbar = xbar; a.w_on = w_on; a.prox_on = prox_on;
+  a.x = x; a.y = y; a.omega = omega; a.status = status; a.iters = iters;
+  a.pobj = pobj; a.dbound = dbound;
+  a.tol = opts ? opts->tol : 1e-9;
+  a.max_iters = opts ? opts->max_iters : 200000;
+  a.check_every = opts ? opts->check_every : 64;
+  a.warm = opts ? opts->warm_start : 1;
+  a.refl = opts ? opts->reflection : 1.0;
+  if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
+  const size_t lds = solve_lds_bytes(b);
+  if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
+  DISPATCH_GEOM(b->block, b->per, {
+    hipLaunchKernelGGL((pdhg_kernel<B_, P_, P_>), dim3(b->S), dim3(B_), lds, b->stream, a);
+  });
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_xbar_accum(ph_batch_t b, const double *x, const double *prob_coeff, int32_t G,
+                  const int32_t *slot_k, const int32_t *slot_s0, const int32_t *slot_s1,
+                  double *out_sums) {
+  if (!b || !x || !prob_coeff || G <= 0 || !slot_k || !slot_s0 || !slot_s1 || !out_sums)
+    return fail(PH_EINVAL, "ph_xbar_accum: bad arguments");
+  if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_xbar_accum: no nonants declared");
+  hipLaunchKernelGGL(xbar_accum_kernel, dim3(G), dim3(256), 0, b->stream, b->S, x, prob_coeff,
+                     b->d_nonant_col, slot_k, slot_s0, slot_s1, G, out_sums);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_update_w(ph_batch_t b, const double *x, const double *sums, int32_t G, const int32_t *gid,
+                const double *rho, const double *w_coeff, double *xbar, double *xsqbar, double *W,
+                double *absdiff) {
+  if (!b || !x || !sums || G <= 0 || !gid || !rho || !xbar || !xsqbar || !absdiff)
+    return fail(PH_EINVAL, "ph_update_w: bad arguments");
+  if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_update_w: no nonants declared");
+  hipLaunchKernelGGL(update_w_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->S,
+                     b->K, x, b->d_nonant_col, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_segment_sum(ph_batch_t b, const double *v, const double *w, int32_t R, const int32_t *seg,
+                   double *out) {
+  if (!b || !v || R <= 0 || !seg || !out) return fail(PH_EINVAL, "ph_segment_sum: bad arguments");
+  hipLaunchKernelGGL(segment_sum_kernel, dim3(R), dim3(256), 0, b->stream, v, w, seg, out);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_eval_objective(ph_batch_t b, const double *x, const double *W, const double *rho,
+                      const double *xbar, double w_on, double prox_on, double *obj) {
+  if (!b || !b->bound || !x || !obj) return fail(PH_EINVAL, "ph_eval_objective: bad arguments");
+  if (b->K && (!W || !rho || !xbar)) return fail(PH_EINVAL, "ph_eval_objective: null W/rho/xbar");
+  hipLaunchKernelGGL(eval_obj_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->S,
+                     b->n, b->d_c, b->d_slot_of_col, x, W, rho, xbar, w_on, prox_on, obj);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_batch_sync(ph_batch_t b) {
+  if (!b) return fail(PH_EINVAL, "null batch");
+  HIP_OK(hipStreamSynchronize(b->stream));
+  return PH_OK;
+}
+
+void ph_batch_destroy(ph_batch_t b) {
+  if (!b) return;
+  void *ptrs[] = {b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k,
+                  b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
+                  b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  delete b;
+}
+
+}  // extern "C"

@@ -1,0 +1,509 @@
+"""PHBase on the MI355X batched solver (mirrors ``mpisppy/phbase.py``).
+
+Method names, argument meanings, option keys and the Iter0 / iterk_loop
+sequencing follow the reference (citations per method).  What changes is
+where the work happens:
+
+* ``solve_loop`` issues ONE batched PDHG launch for all local scenarios
+  (``ph_pdhg_solve``) instead of ``solve_one`` per scenario;
+* W, rho, xbar, xsqbar live in HBM as [K][S] (scenario-fastest) tensors and
+  are updated by device kernels; the per-node Allreduce of Compute_Xbar and
+  the scalar Allreduces of convergence_diff / Ebound / Eobjective become
+  ``torch.distributed`` all_reduce calls (RCCL over xGMI on GPUs).
+"""
+import math
+import time
+import warnings
+
+import numpy as np
+import torch
+
+from . import SOLVER_NAMES, global_toc
+from .spbase import SPBase
+
+# solver option keys understood by the PDHG batch (iter0/iterk_solver_options)
+_PDHG_KEYS = {"pdhg_tol": "tol", "pdhg_max_iters": "max_iters",
+              "pdhg_check_every": "check_every", "warm_start": "warm_start",
+              "pdhg_reflection": "reflection"}
+_DEFAULT_SOLVE = dict(tol=1e-9, max_iters=200000, check_every=64, warm_start=True,
+                      reflection=1.0)
+
+
+class PHBase(SPBase):
+    """Base class for PH on the batched GPU solver.  See ``phbase.py:31-142``."""
+
+    def __init__(self, PHoptions, all_scenario_names, scenario_creator,
+                 scenario_denouement=None, all_nodenames=None, mpicomm=None,
+                 scenario_creator_kwargs=None, PH_extensions=None,
+                 PH_extension_kwargs=None, PH_converger=None, rho_setter=None,
+                 variable_probability=None):
+        super().__init__(PHoptions, all_scenario_names, scenario_creator,
+                         scenario_denouement=scenario_denouement,
+                         all_nodenames=all_nodenames, mpicomm=mpicomm,
+                         scenario_creator_kwargs=scenario_creator_kwargs,
+                         variable_probability=variable_probability)
+        global_toc("Initializing PHBase", self.options.get("verbose", False))
+        self.PHoptions = PHoptions
+        self.options_check()
+        self.PH_extensions = PH_extensions
+        self.PH_extension_kwargs = PH_extension_kwargs
+        self.PH_converger = PH_converger
+        self.rho_setter = rho_setter
+        self.iter0_solver_options = PHoptions["iter0_solver_options"]
+        self.iterk_solver_options = PHoptions["iterk_solver_options"]
+        self.W_disabled = None
+        self.prox_disabled = None
+        self.convobject = None
+        self.conv = None
+        self._PHIter = 0
+        self._prox_approx = False
+        self._duals_attached = False
+        self._prox_attached = False
+        self.w_on = 0.0
+        self.prox_on = 0.0
+        self.batch = None
+        self.device = torch.device("cuda", torch.cuda.current_device()) \
+            if torch.cuda.is_available() else torch.device("cpu")
+        self._warned_keys = set()
+        self.solve_log = []   # (n_scenarios, seconds, mean iters, max iters)
+        self._alloc_state()
+        self.attach_xbars()
+        if self.PH_extensions is not None:
+            if self.PH_extension_kwargs is None:
+                self.extobject = self.PH_extensions(self)
+            else:
+                self.extobject = self.PH_extensions(self, **self.PH_extension_kwargs)
+
+    # ------------------------------------------------------------- state --
+    def _alloc_state(self):
+        d = self.batch_data
+        dev = self.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        K, S = d.K, d.S
+        self.K, self.S_loc = K, S
+        self.prob = torch.as_tensor(self.local_prob, **f64)
+        self.prob_coeff = torch.as_tensor(self.prob_coeff_host.reshape(-1), **f64)
+        self.gid = torch.as_tensor(self.gid_host.reshape(-1), **i32)
+        self.slot_k = torch.as_tensor(self.slot_k_host, **i32)
+        self.slot_s0 = torch.as_tensor(self.slot_s0_host, **i32)
+        self.slot_s1 = torch.as_tensor(self.slot_s1_host, **i32)
+        self.xsums = torch.zeros(2 * self.G, **f64)
+        self.absdiff = torch.zeros(S, **f64)
+        self.obj_buf = torch.zeros(S, **f64)
+        self.seg_all = torch.tensor([0, S], **i32)
+        self.scal = torch.zeros(1, **f64)
+        self.w_coeff = None
+        # convergence_diff: the reference's rank slices (ref_n_proc ranks)
+        R = int(self.PHoptions.get("ref_n_proc", self.n_proc))
+        if R < 1 or R > len(self.all_scenario_names):
+            raise ValueError("ref_n_proc must be in [1, number of scenarios]")
+        from .utils.sputils import rank_slices
+        slices = rank_slices(len(self.all_scenario_names), R)
+        # ref slices are contiguous and cover every scenario (S >= R), so the
+        # local part of ref slice r is [clamp(start_r), clamp(start_{r+1}))
+        seg = [min(max(sl[0], self.local_begin), self.local_end) - self.local_begin
+               for sl in slices]
+        seg.append(self.local_end - self.local_begin)
+        self.ref_n_proc = R
+        self.conv_seg = torch.tensor(seg, **i32)
+        self.conv_cnt = np.array([max(len(sl), 1) * K for sl in slices], dtype=np.float64)
+        self.conv_parts = torch.zeros(R, **f64)
+        self.scenario_feasible = np.ones(S, dtype=bool)
+
+    # ---------------------------------------------------------- options --
+    def options_check(self):
+        """phbase.py:1240-1270."""
+        required = ["solvername", "PHIterLimit", "defaultPHrho", "convthresh", "verbose",
+                    "display_progress", "iter0_solver_options", "iterk_solver_options"]
+        self._options_check(required, self.PHoptions)
+        if "display_timing" not in self.PHoptions:
+            self.PHoptions["display_timing"] = False
+        if "display_convergence_detail" not in self.PHoptions:
+            self.PHoptions["display_convergence_detail"] = False
+        if self.PHoptions["solvername"] not in SOLVER_NAMES:
+            raise ValueError(f"solvername {self.PHoptions['solvername']!r} is not served by "
+                             f"mpisppy_amd; use one of {SOLVER_NAMES}")
+
+    def _solve_kwargs(self, solver_options):
+        kw = dict(_DEFAULT_SOLVE)
+        for k, v in (solver_options or {}).items():
+            if k in _PDHG_KEYS:
+                kw[_PDHG_KEYS[k]] = v
+            elif k not in self._warned_keys:
+                self._warned_keys.add(k)
+                if self.cylinder_rank == 0:
+                    warnings.warn(f"solver option {k}={v} ignored by the PDHG batch solver")
+        return kw
+
+    # ------------------------------------------------- W / prox attach --
+    def attach_xbars(self):
+        """phbase.py:1622-1632."""
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self.xbar = torch.zeros(self.K * self.S_loc, **f64)
+        self.xsqbar = torch.zeros(self.K * self.S_loc, **f64)
+
+    def attach_Ws_and_prox(self):
+        """phbase.py:1110-1131: W=0, rho=defaultPHrho, both terms disabled."""
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self.W = torch.zeros(self.K * self.S_loc, **f64)
+        self.rho = torch.full((self.K * self.S_loc,), float(self.PHoptions["defaultPHrho"]), **f64)
+        self.w_on = 0.0
+        self.prox_on = 0.0
+        self.W_disabled = True
+        self.prox_disabled = True
+
+    def attach_PH_to_objective(self, add_duals=True, add_prox=False):
+        """phbase.py:1133-1209 (the terms are formed inside the solve kernel)."""
+        if self.PHoptions.get("linearize_proximal_terms", False):
+            raise NotImplementedError("linearize_proximal_terms: the GPU solver handles the "
+                                      "exact prox QP; linearization is not supported")
+        self._duals_attached = bool(add_duals)
+        self._prox_attached = bool(add_prox)
+
+    def PH_Prep(self, attach_duals=True, attach_prox=True):
+        """phbase.py:1211-1238."""
+        self.current_solver_options = self.PHoptions["iter0_solver_options"]
+        self.attach_Ws_and_prox()
+        self.attach_PH_to_objective(add_duals=attach_duals, add_prox=attach_prox)
+        if self.PH_extensions is not None:
+            self.extobject.pre_iter0()
+
+    def _set_flags(self):
+        self.w_on = 1.0 if (self._duals_attached and not self.W_disabled) else 0.0
+        self.prox_on = 1.0 if (self._prox_attached and not self.prox_disabled) else 0.0
+
+    def _disable_prox(self):
+        self.prox_disabled = True
+        self._set_flags()
+
+    def _disable_W_and_prox(self):
+        self.prox_disabled = True
+        self.W_disabled = True
+        self._set_flags()
+
+    def _disable_W(self):
+        self.W_disabled = True
+        self._set_flags()
+
+    def _reenable_prox(self):
+        self.prox_disabled = False
+        self._set_flags()
+
+    def _reenable_W_and_prox(self):
+        self.prox_disabled = False
+        self.W_disabled = False
+        self._set_flags()
+
+    def _reenable_W(self):
+        self.W_disabled = False
+        self._set_flags()
+
+    def subproblem_creation(self, verbose=False):
+        """phbase.py:1273-1302 (no bundles: subproblems are the scenarios)."""
+        self.subproblems_created = True
+
+    def _create_solvers(self):
+        """phbase.py:1304-1362: SolverFactory + set_instance  ->  ONE device batch."""
+        if self.batch is not None:
+            return
+        from .batch import DeviceBatch
+        t0 = time.time()
+        self.batch = DeviceBatch(self.batch_data, device=self.device)
+        self.set_instance_time = time.time() - t0
+
+    # ----------------------------------------------------------- solves --
+    def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False,
+                   dtiming=False, dis_W=False, dis_prox=False, gripe=False,
+                   disable_pyomo_signal_handling=False, tee=False, verbose=False):
+        """phbase.py:999-1095: one batched solve of every local subproblem."""
+        if dis_W and dis_prox:
+            self._disable_W_and_prox()
+        elif dis_W:
+            self._disable_W()
+        elif dis_prox:
+            self._disable_prox()
+        if self.batch is None:
+            self._create_solvers()
+        kw = self._solve_kwargs(solver_options)
+        b = self.batch
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
+        torch.cuda.synchronize(self.device)
+        dt = time.perf_counter() - t0
+        status = b.status.cpu().numpy()
+        iters = b.iters.cpu().numpy()
+        self.solve_log.append((self.S_loc, dt, float(iters.mean()), int(iters.max())))
+        self.scenario_feasible = (status == 0) | (status == 1)
+        nlim = int(np.sum(status == 1))
+        if nlim and gripe:
+            print(f"[{type(self).__name__}] {nlim} scenario(s) stopped at the PDHG "
+                  f"iteration limit ({kw['max_iters']})")
+        if gripe and not np.all(self.scenario_feasible):
+            for i in np.nonzero(~self.scenario_feasible)[0]:
+                print(f"[{type(self).__name__}] Solve failed for scenario {self.local_scenario_names[i]}")
+        if dtiming:
+            allt = self.comm.allgather_object(dt)
+            if self.cylinder_rank == 0:
+                print("Pyomo solve times (seconds):")
+                print("\tmin=%4.2f mean=%4.2f max=%4.2f" % (np.min(allt), np.mean(allt), np.max(allt)))
+        if self.PH_extensions is not None and hasattr(self.extobject, "post_solve_loop"):
+            self.extobject.post_solve_loop()
+        if dis_W and dis_prox:
+            self._reenable_W_and_prox()
+        elif dis_W:
+            self._reenable_W()
+        elif dis_prox:
+            self._reenable_prox()
+
+    # ---------------------------------------- nonanticipativity updates --
+    def Compute_Xbar(self, verbose=False):
+        """phbase.py:144-221: weighted node sums, Allreduce, broadcast."""
+        b = self.batch
+        b.xbar_accum(self.prob_coeff, self.slot_k, self.slot_s0, self.slot_s1, self.xsums)
+        self.comm.allreduce_(self.xsums)
+        b.update_w(self.xsums, self.G, self.gid, self.rho, None, self.xbar, self.xsqbar,
+                   None, self.absdiff)
+        if verbose and self.cylinder_rank == 0:
+            print("xbar:", self.xsums[:self.G].cpu().numpy())
+
+    def Update_W(self, verbose):
+        """phbase.py:224-251: W += rho*(x - xbar) (masked by w_coeff if set)."""
+        self.batch.update_w(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
+                            self.xsqbar, self.W, self.absdiff)
+
+    def convergence_diff(self):
+        """phbase.py:254-276: sum over ranks of mean |x - xbar|, / n_proc.
+
+        Reproduces the reference's rank slicing for ``ref_n_proc`` ranks
+        (default: this run's rank count)."""
+        self.batch.segment_sum(self.absdiff, None, self.conv_seg, self.conv_parts)
+        self.comm.allreduce_(self.conv_parts)
+        parts = self.conv_parts.cpu().numpy()
+        return float(np.sum(parts / self.conv_cnt) / self.ref_n_proc)
+
+    def _weighted_sum(self, v):
+        self.batch.segment_sum(v, self.prob, self.seg_all, self.scal)
+        return self.scal
+
+    def Eobjective(self, verbose=False):
+        """phbase.py:279-312: sum_s p_s * (active objective at the current x)."""
+        b = self.batch
+        b.eval_objective(self.W, self.rho, self.xbar, self.w_on, self.prox_on, self.obj_buf)
+        self.obj_buf.add_(b.const)
+        t = self._weighted_sum(self.obj_buf).clone()
+        self.comm.allreduce_(t)
+        v = float(t.item())
+        return v if self.is_minimizing else -v
+
+    def _outer_bounds(self):
+        ob = self.batch.dbound + self.batch.const
+        return ob if self.is_minimizing else -ob
+
+    def Ebound(self, verbose=False, extra_sum_terms=None):
+        """phbase.py:314-354: sum_s p_s * outer_bound_s (+ extra terms)."""
+        ob = self._outer_bounds().contiguous()
+        t = self._weighted_sum(ob).clone()
+        if extra_sum_terms is not None:
+            t = torch.cat([t, torch.tensor(list(extra_sum_terms), dtype=torch.float64,
+                                           device=t.device)])
+        self.comm.allreduce_(t)
+        v = t.cpu().numpy()
+        if extra_sum_terms is None:
+            return float(v[0])
+        return float(v[0]), v[1:]
+
+    def _update_E1(self):
+        """phbase.py:619-636."""
+        self.E1 = self.comm.allreduce_host([float(np.sum(self.local_prob))])[0]
+
+    def feas_prob(self):
+        """phbase.py:649-668."""
+        return self.comm.allreduce_host(
+            [float(np.sum(self.local_prob[self.scenario_feasible]))])[0]
+
+    def infeas_prob(self):
+        return self.comm.allreduce_host(
+            [float(np.sum(self.local_prob[~self.scenario_feasible]))])[0]
+
+    # ---------------------------------------------------------- W I/O --
+    def W_from_flat_list(self, flat_list):
+        """phbase.py:601-617: flat list in (scenario, nonant) order."""
+        a = np.asarray(flat_list, dtype=np.float64).reshape(self.S_loc, self.K)
+        self.W.copy_(torch.as_tensor(a.T.reshape(-1), device=self.device))
+
+    def get_flat_W(self):
+        """Local W as a flat (scenario, nonant)-ordered numpy array."""
+        return self.W.view(self.K, self.S_loc).cpu().numpy().T.reshape(-1)
+
+    def _local_nonant_values(self):
+        x = self.batch.x.view(self.batch.n, self.S_loc)
+        cols = torch.as_tensor(self.batch_data.nonant_cols.astype(np.int64), device=self.device)
+        return x.index_select(0, cols).cpu().numpy()
+
+    def gather_var_values_to_rank0(self):
+        """spbase.py: {(scenario_name, nonant var name): value} on rank 0."""
+        vals = self._local_nonant_values()
+        names = self.nonant_names()
+        local = {(sn, names[k]): float(vals[k, s])
+                 for s, sn in enumerate(self.local_scenario_names) for k in range(self.K)}
+        allv = self.comm.gather_object(local)
+        if self.cylinder_rank != 0:
+            return None
+        out = {}
+        for d in allv:
+            out.update(d)
+        return out
+
+    def report_var_values_at_rank0(self, header="", print_zero_prob_values=False):
+        v = self.gather_var_values_to_rank0()
+        if self.cylinder_rank == 0:
+            print(header)
+            for (sn, vn), val in sorted(v.items()):
+                print(f"  {sn:>20s} {vn:>30s} {val:.6f}")
+
+    def _use_rho_setter(self, verbose):
+        """phbase.py:556-588: rho_setter(model) -> [(vardata, rho)] per scenario."""
+        if self.rho_setter is None:
+            return
+        models = self.batch_data.models
+        if models is None:
+            raise RuntimeError("rho_setter needs per-scenario models (per_scenario_models=True)")
+        from . import repn
+        col2k = {int(c): k for k, c in enumerate(self.batch_data.nonant_cols)}
+        rho = self.rho.view(self.K, self.S_loc)
+        for s, mdl in enumerate(models):
+            for vd, r in self.rho_setter(mdl):
+                rho[col2k[repn.column_of(mdl, vd)], s] = float(r)
+
+    # ----------------------------------------------------------- drivers --
+    def Iter0(self):
+        """phbase.py:1364-1470."""
+        verbose = self.PHoptions["verbose"]
+        dprogress = self.PHoptions["display_progress"]
+        dtiming = self.PHoptions["display_timing"]
+        self._PHIter = 0
+        global_toc("Creating solvers", verbose)
+        self._create_solvers()
+        global_toc("Entering solve loop in PHBase.Iter0", verbose)
+        self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming,
+                        gripe=True, verbose=verbose)
+        self._update_E1()
+        if abs(1 - self.E1) > self.E1_tolerance:
+            raise RuntimeError(f"Total probability of scenarios was {self.E1} "
+                               f"(E1_tolerance = {self.E1_tolerance})")
+        feasP = self.feas_prob()
+        if feasP != self.E1:
+            raise RuntimeError(f"Infeasibility detected; E_feas, E1= {feasP} {self.E1}")
+        if self.PH_extensions is not None:
+            self.extobject.post_iter0()
+        if self.rho_setter is not None:
+            self._use_rho_setter(verbose and self.cylinder_rank == 0)
+        if self.PH_converger is not None:
+            self.convobject = self.PH_converger(self)
+        self.conv = None
+        self.trivial_bound = self.Ebound(verbose)
+        if dprogress and self.cylinder_rank == 0:
+            print("")
+            print("After PH Iteration", self._PHIter)
+            print("Trivial bound =", self.trivial_bound)
+            print("PHBase Convergence Metric =", self.conv)
+            print("Elapsed time: %6.2f" % (time.perf_counter() - self.start_time))
+        if self.PHoptions["display_convergence_detail"]:
+            self.report_var_values_at_rank0(header="Convergence detail:")
+        self._reenable_W_and_prox()
+        self.current_solver_options = self.PHoptions["iterk_solver_options"]
+        return self.trivial_bound
+
+    def iterk_loop(self):
+        """phbase.py:1472-1566: Xbar -> W -> conv -> [hub] -> break? -> solve."""
+        verbose = self.PHoptions["verbose"]
+        have_extensions = self.PH_extensions is not None
+        have_converger = self.PH_converger is not None
+        dprogress = self.PHoptions["display_progress"]
+        dtiming = self.PHoptions["display_timing"]
+        self.conv = None
+        max_iterations = int(self.PHoptions["PHIterLimit"])
+        self.conv_history = []
+        for self._PHIter in range(1, max_iterations + 1):
+            iteration_start_time = time.time()
+            if dprogress:
+                global_toc(f"\nInitiating PH Iteration {self._PHIter}\n", self.cylinder_rank == 0)
+            self.Compute_Xbar(verbose)
+            self.Update_W(verbose)
+            self.conv = self.convergence_diff()
+            self.conv_history.append(self.conv)
+            if have_extensions:
+                self.extobject.miditer()
+            if self.spcomm is not None:
+                self.spcomm.sync()
+                if self.spcomm.is_converged():
+                    global_toc("Cylinder convergence", self.cylinder_rank == 0)
+                    break
+            if have_converger:
+                if self.convobject.is_converged():
+                    global_toc("User-supplied converger determined termination criterion reached",
+                               self.cylinder_rank == 0)
+                    break
+            elif self.conv is not None:
+                if self.conv < self.PHoptions["convthresh"]:
+                    global_toc("Convergence metric=%f dropped below user-supplied threshold=%f"
+                               % (self.conv, self.PHoptions["convthresh"]),
+                               self.cylinder_rank == 0 and (verbose or dprogress))
+                    break
+            self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming,
+                            gripe=True, verbose=verbose)
+            if have_extensions:
+                self.extobject.enditer()
+            if dprogress and self.cylinder_rank == 0:
+                print("")
+                print("After PH Iteration", self._PHIter)
+                print("Scaled PHBase Convergence Metric=", self.conv)
+                print("Iteration time: %6.2f" % (time.time() - iteration_start_time))
+                print("Elapsed time:   %6.2f" % (time.perf_counter() - self.start_time))
+            if self.PHoptions["display_convergence_detail"]:
+                self.report_var_values_at_rank0(header="Convergence detail:")
+            if self._PHIter == max_iterations:
+                global_toc("Reached user-specified limit=%d on number of PH iterations"
+                           % max_iterations, self.cylinder_rank == 0 and (verbose or dprogress))
+
+    def post_loops(self, PH_extensions=None):
+        """phbase.py:1568-1620."""
+        dprogress = self.PHoptions["display_progress"]
+        self.comm.Barrier()
+        if self.scenario_denouement is not None:
+            for sname, s in self.local_scenarios.items():
+                self.scenario_denouement(self.cylinder_rank, sname, s)
+        self.comm.Barrier()
+        if PH_extensions is not None:
+            self.extobject.post_everything()
+        Eobj = self.Eobjective(self.PHoptions["verbose"])
+        self.comm.Barrier()
+        if dprogress and self.cylinder_rank == 0:
+            print("")
+            print("Current ***weighted*** E[objective] =", Eobj)
+            print("")
+        return Eobj
+
+    def post_solve_bound(self, solver_options=None, verbose=False):
+        """phbase.py:753-801: W on, prox off, LP solves, Ebound."""
+        if self.cylinder_rank == 0:
+            print("Warning: Lagrangian bounds might not be correct in certain "
+                  "cases where there are integers not subject to "
+                  "non-anticipativity and those integers do not reach integrality.")
+        if self.W_disabled:
+            self._reenable_W()
+        self._disable_prox()
+        self.solve_loop(solver_options=solver_options, dis_prox=False, gripe=True,
+                        tee=False, verbose=verbose)
+        bound = self.Ebound(verbose)
+        self._reenable_prox()
+        return bound
+
+    # ----------------------------------------------------------- metrics --
+    def solves_per_second(self):
+        """Scenario subproblem solves per second of solve_loop wall time (local)."""
+        n = sum(x[0] for x in self.solve_log)
+        t = sum(x[1] for x in self.solve_log)
+        return n / t if t > 0 else math.nan
