@@ -227,10 +227,10 @@ class PHBase(SPBase):
             self._create_solvers()
         kw = self._solve_kwargs(solver_options)
         b = self.batch
-        torch.cuda.synchronize(self.device)
+        self._sync()
         t0 = time.perf_counter()
         b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
-        torch.cuda.synchronize(self.device)
+        self._sync()
         dt = time.perf_counter() - t0
         status = b.status.cpu().numpy()
         iters = b.iters.cpu().numpy()
@@ -256,6 +256,10 @@ class PHBase(SPBase):
             self._reenable_W()
         elif dis_prox:
             self._reenable_prox()
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     # ---------------------------------------- nonanticipativity updates --
     def Compute_Xbar(self, verbose=False):

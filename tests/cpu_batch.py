@@ -1,0 +1,85 @@
+"""Test-only stand-in for DeviceBatch on CPU tensors.
+
+Implements the five device operations PHBase calls (solve, xbar_accum,
+update_w, segment_sum, eval_objective) with torch CPU ops and the oracle's
+exact per-scenario solver, so the distributed *host* logic of PHBase
+(slicing, node slots, allreduces, convergence bookkeeping) can be tested
+with gloo on a machine without a GPU.  Never used by the product.
+"""
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from oracle.solve import solve_scenario
+
+
+class CPUBatch:
+    def __init__(self, data):
+        self.data = data
+        self.S, self.n, self.m, self.nnz, self.K = data.S, data.n, data.m, data.nnz, data.K
+        f64 = dict(dtype=torch.float64)
+        self.x = torch.zeros(self.n * self.S, **f64)
+        self.y = torch.zeros(max(self.m, 1) * self.S, **f64)
+        self.status = torch.zeros(self.S, dtype=torch.int32)
+        self.iters = torch.zeros(self.S, dtype=torch.int32)
+        self.pobj = torch.zeros(self.S, **f64)
+        self.dbound = torch.zeros(self.S, **f64)
+        self.const = torch.as_tensor(data.const, **f64)
+        self.cols = torch.as_tensor(data.nonant_cols.astype(np.int64))
+
+    def _A(self, s):
+        d = self.data
+        return sp.csr_matrix((d.vals[:, s], d.col_idx, d.row_ptr), shape=(d.m, d.n))
+
+    def solve(self, W, rho, xbar, w_on, prox_on, **kw):
+        d = self.data
+        Wv = W.view(self.K, self.S).numpy(); rv = rho.view(self.K, self.S).numpy()
+        xb = xbar.view(self.K, self.S).numpy()
+        X = self.x.view(self.n, self.S)
+        for s in range(self.S):
+            g = d.c[:, s].copy(); q = np.zeros(self.n)
+            g[d.nonant_cols] += w_on * Wv[:, s] - prox_on * rv[:, s] * xb[:, s]
+            q[d.nonant_cols] += prox_on * rv[:, s]
+            cst = prox_on * float(np.sum(rv[:, s] / 2 * xb[:, s] ** 2))
+            x, y, feas = solve_scenario(g, q, self._A(s), d.rl[:, s], d.ru[:, s], d.l[:, s], d.u[:, s])
+            X[:, s] = torch.as_tensor(x)
+            v = 0.5 * float(q @ (x * x)) + float(g @ x) + cst
+            self.pobj[s] = v
+            self.dbound[s] = v
+            self.status[s] = 0
+
+    def xbar_accum(self, prob_coeff, slot_k, slot_s0, slot_s1, out):
+        X = self.x.view(self.n, self.S)[self.cols]
+        pc = prob_coeff.view(self.K, self.S)
+        G = slot_k.numel()
+        for g in range(G):
+            k, a, b = int(slot_k[g]), int(slot_s0[g]), int(slot_s1[g])
+            out[g] = (pc[k, a:b] * X[k, a:b]).sum()
+            out[G + g] = (pc[k, a:b] * X[k, a:b] ** 2).sum()
+
+    def update_w(self, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff):
+        X = self.x.view(self.n, self.S)[self.cols]
+        gi = gid.view(self.K, self.S).long()
+        xb = sums[:G][gi]
+        xbar.view(self.K, self.S).copy_(xb)
+        xsqbar.view(self.K, self.S).copy_(sums[G:][gi])
+        d = X - xb
+        if W is not None:
+            Wv = W.view(self.K, self.S)
+            Wv.add_(rho.view(self.K, self.S) * d)
+            if w_coeff is not None:
+                Wv.mul_(w_coeff.view(self.K, self.S))
+        absdiff.copy_(d.abs().sum(0))
+
+    def segment_sum(self, v, w, seg, out):
+        for r in range(seg.numel() - 1):
+            a, b = int(seg[r]), int(seg[r + 1])
+            out[r] = (v[a:b] * (w[a:b] if w is not None else 1.0)).sum()
+
+    def eval_objective(self, W, rho, xbar, w_on, prox_on, out):
+        d = self.data
+        X = self.x.view(self.n, self.S)
+        out.copy_((torch.as_tensor(d.c) * X).sum(0))
+        Xn = X[self.cols]
+        Wv = W.view(self.K, self.S); rv = rho.view(self.K, self.S); xb = xbar.view(self.K, self.S)
+        out.add_((w_on * Wv * Xn + prox_on * 0.5 * rv * (Xn ** 2 - 2 * xb * Xn + xb ** 2)).sum(0))

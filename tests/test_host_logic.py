@@ -1,0 +1,132 @@
+"""PHBase host logic on CPU: slicing, node slots, and the full PH control flow
+driven through a CPU stand-in batch, single rank and 2-rank gloo."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import models as om
+from oracle.ph_oracle import OraclePH
+
+
+def _opts(**kw):
+    o = {"solvername": "mi355x_pdhg", "PHIterLimit": 6, "defaultPHrho": 1.0,
+         "convthresh": 1e-9, "verbose": False, "display_progress": False,
+         "display_timing": False, "iter0_solver_options": {}, "iterk_solver_options": {}}
+    o.update(kw)
+    return o
+
+
+def _run_ph(opts, names, creator, kw=None, nodes=None, mpicomm=None):
+    from mpisppy_amd.opt.ph import PH
+    from cpu_batch import CPUBatch
+    ph = PH(dict(opts), names, creator, all_nodenames=nodes, mpicomm=mpicomm,
+            scenario_creator_kwargs=kw)
+    ph.batch = CPUBatch(ph.batch_data)
+    conv, eobj, tb = ph.ph_main()
+    return ph, conv, eobj, tb
+
+
+def test_spbase_slices_and_probabilities():
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import hydro
+    names, nodes = hydro.all_names_and_nodes()
+    ph = PH(_opts(branching_factors=[3, 3]), names, hydro.scenario_creator, all_nodenames=nodes,
+            scenario_creator_kwargs={"branching_factors": [3, 3]})
+    assert ph.G == 16                        # ROOT(4) + 3 x ROOT_b(4)
+    pc = ph.prob_coeff_host
+    assert np.allclose(pc[:4], 1 / 9) and np.allclose(pc[4:], 1 / 3)   # spbase.py:353-366
+    assert list(ph.slot_s0_host[4:8]) == [0] * 4 and list(ph.slot_s1_host[4:8]) == [3] * 4
+    assert list(ph.slot_s0_host[12:16]) == [6] * 4
+
+
+def test_farmer_ph_host_flow_matches_oracle_single_rank():
+    from mpisppy_amd.examples import farmer
+    S = 6
+    names = [f"scen{i}" for i in range(S)]
+    ph, conv, eobj, tb = _run_ph(_opts(), names, farmer.scenario_creator)
+    orc = OraclePH(_opts(), [om.farmer(n) for n in names])
+    oc, oe, ot = orc.ph_main()
+    assert abs(tb - ot) < 1e-9 * abs(ot)
+    assert abs(eobj - oe) < 1e-9 * abs(oe)
+    assert abs(conv - oc) < 1e-9 * abs(oc)
+    W = ph.W.view(ph.K, ph.S_loc).numpy().T
+    assert np.allclose(W, np.array(orc.W), rtol=1e-9, atol=1e-9)
+
+
+def test_hydro_ph_host_flow_matches_oracle():
+    from mpisppy_amd.examples import hydro
+    names, nodes = hydro.all_names_and_nodes()
+    opts = _opts(PHIterLimit=10, convthresh=1e-3, branching_factors=[3, 3])
+    ph, conv, eobj, tb = _run_ph(opts, names, hydro.scenario_creator,
+                                 kw={"branching_factors": [3, 3]}, nodes=nodes)
+    orc = OraclePH(opts, [om.hydro(n) for n in names])
+    oc, oe, ot = orc.ph_main()
+    assert ph._PHIter == orc.iters
+    assert abs(tb - ot) < 1e-8 * abs(ot)
+    assert abs(eobj - oe) < 1e-8 * abs(oe)
+
+
+def test_ref_n_proc_emulates_reference_rank_count():
+    from mpisppy_amd.examples import farmer
+    names = [f"scen{i}" for i in range(7)]
+    ph, conv, _, _ = _run_ph(_opts(PHIterLimit=3, ref_n_proc=3), names, farmer.scenario_creator)
+    orc = OraclePH(_opts(PHIterLimit=3), [om.farmer(n) for n in names], n_proc=3)
+    oc, _, _ = orc.ph_main()
+    assert abs(conv - oc) < 1e-9 * abs(oc)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "mpi-sppy_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mpisppy_amd.examples import hydro
+        names, nodes = hydro.all_names_and_nodes()
+        opts = _opts(PHIterLimit=10, convthresh=1e-3, branching_factors=[3, 3])
+        ph, conv, eobj, tb = _run_ph(opts, names, hydro.scenario_creator,
+                                     kw={"branching_factors": [3, 3]}, nodes=nodes)
+        q.put((rank, conv, eobj, tb, ph._PHIter, ph.local_scenario_names))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_two_rank_gloo_hydro_matches_oracle():
+    """Scenarios split 4/5 over 2 ranks (the reference's slicing); per-node
+    xbar sums, conv and bounds go through gloo allreduce."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert res[0][5] == [f"Scen{i}" for i in range(1, 5)]
+    assert res[1][5] == [f"Scen{i}" for i in range(5, 10)]
+    opts = _opts(PHIterLimit=10, convthresh=1e-3)
+    orc = OraclePH(opts, [om.hydro(f"Scen{i + 1}") for i in range(9)], n_proc=2)
+    oc, oe, ot = orc.ph_main()
+    for rank, conv, eobj, tb, iters, _ in res:
+        assert iters == orc.iters
+        assert abs(conv - oc) < 1e-8 * abs(oc)
+        assert abs(eobj - oe) < 1e-8 * abs(oe)
+        assert abs(tb - ot) < 1e-8 * abs(ot)
