@@ -68,6 +68,18 @@ def cpu_baseline(c, sample_scens, rank):
 
 
 def main():
+    # everything but the final JSON line goes to stderr
+    real_stdout = sys.stdout
+    sys.stdout = sys.stderr
+    try:
+        out = run()
+    finally:
+        sys.stdout = real_stdout
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+def run():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -221,9 +233,11 @@ def main():
             "ph_to_tol": tol_info,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+    else:
+        out = None
     if world > 1:
         dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":

@@ -154,6 +154,13 @@ int ph_eval_objective(ph_batch_t b, const double *x, const double *W,
                       const double *rho, const double *xbar, double w_on,
                       double prox_on, double *obj);
 
+/*
+ * Diagnostics of the last ph_pdhg_solve, copied to host out[4*S]:
+ * per scenario the final relative primal residual, dual residual, duality
+ * gap and Halpern fixed-point residual (synchronises the stream).
+ */
+int ph_batch_get_diag(ph_batch_t b, double *out /*host [S][4]*/);
+
 /* Block until all work queued on the batch's stream has finished. */
 int ph_batch_sync(ph_batch_t b);
 

@@ -216,6 +216,7 @@ struct SolveArgs {
   double *x, *y, *omega;
   int32_t *status, *iters;
   double *pobj, *dbound;
+  double *diag;  // [S][4]: final ep, ed, eg, r (library-owned)
   double tol;
   int max_iters, check_every, warm;
   double refl;
@@ -295,14 +296,18 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     }
   }
   // initial primal weight, objective constant
-  double omega;
+  double omega, omega0;
   {
     double v[3] = {cst, gsq, bsq};
     block_sum<3>(v, red);
     cst = v[0];
     double gn = sqrt(v[1]), bn = sqrt(v[2]);
-    omega = (gn > 1e-10 && bn > 1e-10) ? gn / bn : 1.0;
-    if (a.warm && a.omega[s] > 0.0) omega = a.omega[s];
+    omega0 = (gn > 1e-10 && bn > 1e-10) ? gn / bn : 1.0;
+    omega = omega0;
+    // warm primal weight, kept within 100x of the data-based weight: carried
+    // unclamped across PH iterations it drifts (1e6x seen on farmer) into a
+    // regime where FP64 round-off stalls the iteration above 1e-9.
+    if (a.warm && a.omega[s] > 0.0) omega = clampd(a.omega[s], omega0 * 1e-2, omega0 * 1e2);
   }
   const double eta = a.eta[s];
   const double gam = a.refl;
@@ -335,6 +340,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   int stat = PH_STATUS_ITERLIMIT;
   double r_restart = -1.0, r_prev = -1.0;
   double out_pobj = 0.0, out_dobj = 0.0;
+  double d_ep = -1.0, d_ed = -1.0, d_eg = -1.0, d_r = -1.0;
   const int maxit = a.max_iters;
   const int chk = a.check_every > 0 ? a.check_every : 64;
 
@@ -446,6 +452,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     out_pobj = P0;
     out_dobj = D0;
     const double r = sqrt(omega * v[8] + v[9] / omega);
+    d_ep = ep; d_ed = ed; d_eg = eg; d_r = r;
     if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
       stat = PH_STATUS_OPTIMAL;
 #pragma unroll
@@ -463,9 +470,20 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
                 (k >= 0.36 * (double)(it + 1));
     }
     r_prev = r;
-    if (restart) {
+    // safeguard: every 8192 steps, a primal weight that has drifted more than
+    // 100x from the data-based weight is reset (seen stalling on farmer warm
+    // starts at ~1e-8 relative KKT, in both directions)
+    const bool reset = it > 0 && ((it + 1) % 8192) < chk &&
+                       (omega > 1e2 * omega0 || omega < 1e-2 * omega0);
+    if (reset) {
+      omega = omega0;
+      restart = true;
+    } else if (restart) {
+      // PDLP primal weight update, smoothing 0.5
       const double dx = sqrt(v[4]), dy = sqrt(v[5]);
       if (dx > 1e-12 && dy > 1e-12) omega = exp(0.5 * log(dy / dx) + 0.5 * log(omega));
+    }
+    if (restart) {
 #pragma unroll
       for (int b = 0; b < CPT; ++b) X[b] = Z0X[b] = XN[b];
 #pragma unroll
@@ -502,6 +520,10 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     a.iters[s] = it;
     a.pobj[s] = out_pobj;
     a.dbound[s] = out_dobj;
+    a.diag[4 * s + 0] = d_ep;
+    a.diag[4 * s + 1] = d_ed;
+    a.diag[4 * s + 2] = d_eg;
+    a.diag[4 * s + 3] = d_r;
   }
 }
 
@@ -604,6 +626,7 @@ struct ph_batch {
   int32_t *d_slot_of_col = nullptr, *d_nonant_col = nullptr;
   double *d_vals_s = nullptr, *d_dr = nullptr, *d_dc = nullptr, *d_eta = nullptr;
   double *d_c = nullptr, *d_l = nullptr, *d_u = nullptr, *d_rl = nullptr, *d_ru = nullptr;
+  double *d_diag = nullptr;
   bool bound = false;
   int per = 1, block = 64;
 };
@@ -688,7 +711,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_dc, (size_t)S * n)) || (rc = dalloc(&b->d_eta, S)) ||
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
-      (rc = dalloc(&b->d_ru, (size_t)S * m))) {
+      (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * 4))) {
     ph_batch_destroy(b);
     return rc;
   }
@@ -782,7 +805,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.slot_of_col = b->d_slot_of_col;
   a.W = W; a.rho = rho; a.xbar = xbar; a.w_on = w_on; a.prox_on = prox_on;
   a.x = x; a.y = y; a.omega = omega; a.status = status; a.iters = iters;
-  a.pobj = pobj; a.dbound = dbound;
+  a.pobj = pobj; a.dbound = dbound; a.diag = b->d_diag;
   a.tol = opts ? opts->tol : 1e-9;
   a.max_iters = opts ? opts->max_iters : 200000;
   a.check_every = opts ? opts->check_every : 64;
@@ -840,6 +863,13 @@ int ph_eval_objective(ph_batch_t b, const double *x, const double *W, const doub
   return PH_OK;
 }
 
+int ph_batch_get_diag(ph_batch_t b, double *out) {
+  if (!b || !out) return fail(PH_EINVAL, "ph_batch_get_diag: bad arguments");
+  HIP_OK(hipMemcpyAsync(out, b->d_diag, sizeof(double) * 4 * (size_t)b->S, hipMemcpyDeviceToHost, b->stream));
+  HIP_OK(hipStreamSynchronize(b->stream));
+  return PH_OK;
+}
+
 int ph_batch_sync(ph_batch_t b) {
   if (!b) return fail(PH_EINVAL, "null batch");
   HIP_OK(hipStreamSynchronize(b->stream));
@@ -850,7 +880,7 @@ void ph_batch_destroy(ph_batch_t b) {
   if (!b) return;
   void *ptrs[] = {b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k,
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
-                  b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru};
+                  b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete b;

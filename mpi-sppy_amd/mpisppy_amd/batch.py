@@ -218,6 +218,13 @@ class DeviceBatch:
                                                  _native.ptr(rho), _native.ptr(xbar), float(w_on),
                                                  float(prox_on), _native.ptr(out)), "ph_eval_objective")
 
+    def diagnostics(self):
+        """[S][4] host array: final (primal res, dual res, gap, fixed-point res)."""
+        out = np.zeros((self.S, 4))
+        _native.check(self.lib.ph_batch_get_diag(self.handle, out.ctypes.data_as(_native._c_ptr)),
+                      "ph_batch_get_diag")
+        return out
+
     def x_host(self):
         return self.x.view(self.n, self.S).cpu().numpy()
 
