@@ -225,7 +225,7 @@ struct SolveArgs {
 // ------------------------------------------------------------------------
 // PDHG solve kernel: one workgroup per scenario, everything on chip.
 // ------------------------------------------------------------------------
-template <int BLOCK, int CPT, int RPT>
+template <int BLOCK, int CPT, int RPT, int MAXD>
 __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int s = blockIdx.x;
@@ -239,6 +239,74 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
 
   const double *vs = a.vals_s + (size_t)s * nnz;
   for (int k = tid; k < nnz; k += T) vals[k] = vs[k];
+
+  // ---- this thread's matrix entries, cached in VGPRs (index + scaled value)
+  // so each SpMV / SpMV^T step issues only independent LDS loads of the
+  // shared vector; columns/rows longer than MAXD use the pattern loop.
+  int CN[CPT], CB[CPT], CR[CPT][MAXD];
+  double CV[CPT][MAXD];
+  int RN[RPT], RB[RPT], RC[RPT][MAXD];
+  double RV[RPT][MAXD];
+#pragma unroll
+  for (int b = 0; b < CPT; ++b) {
+    int j = tid + b * T;
+    CN[b] = 0;
+    CB[b] = 0;
+    if (j < n) {
+      CB[b] = a.P.col_ptr[j];
+      CN[b] = a.P.col_ptr[j + 1] - CB[b];
+    }
+#pragma unroll
+    for (int e = 0; e < MAXD; ++e) {
+      CR[b][e] = 0;
+      CV[b][e] = 0.0;
+      if (e < CN[b]) {
+        CR[b][e] = a.P.csc_row[CB[b] + e];
+        CV[b][e] = vs[a.P.csc_k[CB[b] + e]];
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < RPT; ++b) {
+    int i = tid + b * T;
+    RN[b] = 0;
+    RB[b] = 0;
+    if (i < m) {
+      RB[b] = a.P.row_ptr[i];
+      RN[b] = a.P.row_ptr[i + 1] - RB[b];
+    }
+#pragma unroll
+    for (int e = 0; e < MAXD; ++e) {
+      RC[b][e] = 0;
+      RV[b][e] = 0.0;
+      if (e < RN[b]) {
+        RC[b][e] = a.P.col_idx[RB[b] + e];
+        RV[b][e] = vs[RB[b] + e];
+      }
+    }
+  }
+  // (A^T v)_j for owned column slot b, v in LDS
+  auto coldot = [&](int b, const double *v) -> double {
+    double acc = 0.0;
+    if (CN[b] <= MAXD) {  // padded entries carry value 0 and index 0
+#pragma unroll
+      for (int e = 0; e < MAXD; ++e) acc += CV[b][e] * v[CR[b][e]];
+    } else {
+      for (int p = CB[b]; p < CB[b] + CN[b]; ++p) acc += vals[a.P.csc_k[p]] * v[a.P.csc_row[p]];
+    }
+    return acc;
+  };
+  // (A v)_i for owned row slot b, v in LDS
+  auto rowdot = [&](int b, const double *v) -> double {
+    double acc = 0.0;
+    if (RN[b] <= MAXD) {
+#pragma unroll
+      for (int e = 0; e < MAXD; ++e) acc += RV[b][e] * v[RC[b][e]];
+    } else {
+      for (int p = RB[b]; p < RB[b] + RN[b]; ++p) acc += vals[p] * v[a.P.col_idx[p]];
+    }
+    return acc;
+  };
 
   // ---- column state in registers
   double X[CPT], Z0X[CPT], G[CPT], Q[CPT], L[CPT], U[CPT], DC[CPT], XN[CPT];
@@ -327,11 +395,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
 #pragma unroll
   for (int b = 0; b < RPT; ++b) {
     int i = tid + b * T;
-    if (i < m) {
-      double acc = 0.0;
-      for (int p = a.P.row_ptr[i]; p < a.P.row_ptr[i + 1]; ++p) acc += vals[p] * xs[a.P.col_idx[p]];
-      AX[b] = AZ0[b] = acc;
-    }
+    if (i < m) AX[b] = AZ0[b] = rowdot(b, xs);
   }
   __syncthreads();
 
@@ -344,10 +408,20 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   const int maxit = a.max_iters;
   const int chk = a.check_every > 0 ? a.check_every : 64;
 
+  // step sizes change only with the primal weight: no FP64 division in the
+  // iteration except the Halpern weight 1/(k+2)
+  double tau = 0.0, sig = 0.0, IQ[CPT];
+  auto set_steps = [&]() {
+    tau = eta / omega;
+    sig = eta * omega;
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) IQ[b] = 1.0 / (1.0 + tau * Q[b]);
+  };
+  set_steps();
+
   for (it = 0; it < maxit; ++it) {
-    const double tau = eta / omega, sig = eta * omega;
-    const double ca = (double)(k + 1) / (double)(k + 2);
     const double cb = 1.0 / (double)(k + 2);
+    const double ca = (double)(k + 1) * cb;
     const bool check = (it % chk) == 0 || it == maxit - 1;
     double dxx = 0.0, dyy = 0.0;
 
@@ -356,10 +430,8 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     for (int b = 0; b < CPT; ++b) {
       int j = tid + b * T;
       if (j < n) {
-        double aty = 0.0;
-        for (int p = a.P.col_ptr[j]; p < a.P.col_ptr[j + 1]; ++p)
-          aty += vals[a.P.csc_k[p]] * ys[a.P.csc_row[p]];
-        double xn = clampd((X[b] - tau * (G[b] - aty)) / (1.0 + tau * Q[b]), L[b], U[b]);
+        const double aty = coldot(b, ys);
+        double xn = clampd((X[b] - tau * (G[b] - aty)) * IQ[b], L[b], U[b]);
         double d = xn - X[b];
         dxx += d * d;
         XN[b] = xn;
@@ -373,9 +445,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     for (int b = 0; b < RPT; ++b) {
       int i = tid + b * T;
       if (i < m) {
-        double axn = 0.0;
-        for (int p = a.P.row_ptr[i]; p < a.P.row_ptr[i + 1]; ++p)
-          axn += vals[p] * xs[a.P.col_idx[p]];
+        const double axn = rowdot(b, xs);
         double v = Y[b] - sig * (2.0 * axn - AX[b]);
         double yn = fmax(v + sig * RL[b], 0.0) + fmin(v + sig * RU[b], 0.0);
         double d = yn - Y[b];
@@ -409,9 +479,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     for (int b = 0; b < CPT; ++b) {
       int j = tid + b * T;
       if (j < n) {
-        double aty = 0.0;
-        for (int p = a.P.col_ptr[j]; p < a.P.col_ptr[j + 1]; ++p)
-          aty += vals[a.P.csc_k[p]] * ys[a.P.csc_row[p]];
+        const double aty = coldot(b, ys);
         double lam = (Q[b] * XN[b] + G[b] - aty) / DC[b];  // unscaled reduced cost
         double xu = XN[b] * DC[b];
         double lu = L[b] * DC[b], uu = U[b] * DC[b];
@@ -484,6 +552,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
       if (dx > 1e-12 && dy > 1e-12) omega = exp(0.5 * log(dy / dx) + 0.5 * log(omega));
     }
     if (restart) {
+      set_steps();
 #pragma unroll
       for (int b = 0; b < CPT; ++b) X[b] = Z0X[b] = XN[b];
 #pragma unroll
@@ -628,7 +697,7 @@ struct ph_batch {
   double *d_c = nullptr, *d_l = nullptr, *d_u = nullptr, *d_rl = nullptr, *d_ru = nullptr;
   double *d_diag = nullptr;
   bool bound = false;
-  int per = 1, block = 64;
+  int per = 1, block = 64, maxd = 4;
 };
 
 namespace {
@@ -701,8 +770,17 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
   ph_batch *b = new ph_batch();
   b->S = S; b->n = n; b->m = m; b->nnz = nnz;
   b->stream = (hipStream_t)stream;
+  {  // register-cached entries per row/column: 4 when >= 95% of them fit, else 8
+    int fit4 = 0;
+    for (int i = 0; i < m; ++i) fit4 += (row_ptr[i + 1] - row_ptr[i]) <= 4;
+    for (int j = 0; j < n; ++j) fit4 += (col_ptr[j + 1] - col_ptr[j]) <= 4;
+    b->maxd = (fit4 >= 0.95 * (n + m)) ? 4 : 8;
+  }
   if (!pick_geometry(n, m, &b->block, &b->per))
+  {
+    delete b;
     return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns; the on-chip PDHG kernel does not cover it");
+  }
   int rc = 0;
   if ((rc = dalloc(&b->d_row_ptr, m + 1)) || (rc = dalloc(&b->d_col_idx, nnz)) ||
       (rc = dalloc(&b->d_col_ptr, n + 1)) || (rc = dalloc(&b->d_csc_row, nnz)) ||
@@ -814,9 +892,15 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
-  DISPATCH_GEOM(b->block, b->per, {
-    hipLaunchKernelGGL((pdhg_kernel<B_, P_, P_>), dim3(b->S), dim3(B_), lds, b->stream, a);
-  });
+  if (b->maxd <= 4) {
+    DISPATCH_GEOM(b->block, b->per, {
+      hipLaunchKernelGGL((pdhg_kernel<B_, P_, P_, 4>), dim3(b->S), dim3(B_), lds, b->stream, a);
+    });
+  } else {
+    DISPATCH_GEOM(b->block, b->per, {
+      hipLaunchKernelGGL((pdhg_kernel<B_, P_, P_, 8>), dim3(b->S), dim3(B_), lds, b->stream, a);
+    });
+  }
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
