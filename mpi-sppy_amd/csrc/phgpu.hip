@@ -85,6 +85,20 @@ struct Pattern {
   const int32_t *csc_k;    // [nnz]  CSR position of CSC entry
 };
 
+// Entries per line held in registers by the line's owner; longer lines are
+// cut into extra chunks of LINE_D (see LineRegs).
+constexpr int LINE_D = 4;
+
+struct Chunks {
+  int xr, xc;              // number of extra row / column chunks
+  const int32_t *r_pb;     // [m+1] row i's partials are [r_pb[i], r_pb[i+1])
+  const int32_t *r_pos;    // [xr] CSR position of the chunk's first entry
+  const int32_t *r_len;    // [xr] entries in the chunk (<= LINE_D)
+  const int32_t *c_pb;     // [n+1]
+  const int32_t *c_pos;    // [xc] CSC position
+  const int32_t *c_len;    // [xc]
+};
+
 // ------------------------------------------------------------------------
 // Scaling kernel: per scenario Ruiz (10 sweeps) + Pock-Chambolle(alpha=1),
 // writes dr [S][m], dc [S][n], scaled values [S][nnz] and the step size
@@ -208,6 +222,7 @@ __global__ void __launch_bounds__(BLOCK) scale_kernel(
 struct SolveArgs {
   int S, n, m, nnz;
   Pattern P;
+  Chunks X;
   const double *vals_s, *dr, *dc, *eta;
   const double *c, *l, *u, *rl, *ru;
   const int32_t *slot_of_col;
@@ -222,91 +237,130 @@ struct SolveArgs {
   double refl;
 };
 
+// Matrix entries a thread keeps in VGPRs for the lines (rows or columns) it
+// owns plus the extra chunks of long lines it helps with.  A line's first
+// LINE_D entries belong to its owner; entries beyond that are cut into
+// chunks of LINE_D, numbered globally, spread over the block (chunk q is
+// slot q / T of thread q % T) and summed into LDS partials part[q].  The
+// owner adds its line's partials [pb, pb+pn).  Padded entries carry value 0
+// and index 0, so every dot product is a fixed LINE_D-term unrolled FMA chain.
+template <int P, int E>
+struct LineRegs {
+  int idx[P][LINE_D];
+  double val[P][LINE_D];
+  int pb[P], pn[P];
+  int xidx[E > 0 ? E : 1][LINE_D];
+  double xval[E > 0 ? E : 1][LINE_D];
+  bool xon[E > 0 ? E : 1];
+
+  // own line `line` (or nothing when line >= nlines); entries at pattern
+  // positions [beg, end); entry p has index ix[p] and value v[vk ? vk[p] : p]
+  __device__ __forceinline__ void load_own(int b, int line, int nlines, const int32_t *ptr,
+                                           const int32_t *ix, const int32_t *vk,
+                                           const double *v, const int32_t *xpb) {
+    pb[b] = 0;
+    pn[b] = 0;
+    int beg = 0, len = 0;
+    if (line < nlines) {
+      beg = ptr[line];
+      len = ptr[line + 1] - beg;
+      if (xpb) {
+        pb[b] = xpb[line];
+        pn[b] = xpb[line + 1] - pb[b];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < LINE_D; ++e) {
+      idx[b][e] = 0;
+      val[b][e] = 0.0;
+      if (e < len) {
+        const int p = beg + e;
+        idx[b][e] = ix[p];
+        val[b][e] = v[vk ? vk[p] : p];
+      }
+    }
+  }
+  __device__ __forceinline__ void load_extra(int e, int q, int nx, const int32_t *xpos,
+                                             const int32_t *xlen, const int32_t *ix,
+                                             const int32_t *vk, const double *v) {
+    xon[e] = q < nx;
+    int beg = 0, len = 0;
+    if (xon[e]) {
+      beg = xpos[q];
+      len = xlen[q];
+    }
+#pragma unroll
+    for (int d = 0; d < LINE_D; ++d) {
+      xidx[e][d] = 0;
+      xval[e][d] = 0.0;
+      if (d < len) {
+        const int p = beg + d;
+        xidx[e][d] = ix[p];
+        xval[e][d] = v[vk ? vk[p] : p];
+      }
+    }
+  }
+  // out[b] = (line b of the matrix) . vec for every owned line.  Contains one
+  // block barrier when E > 0 (partials), none otherwise; vec must be complete
+  // in LDS before the call and part[] is free to overwrite.
+  __device__ __forceinline__ void dots(const double *vec, double *part, double (&out)[P]) {
+    if constexpr (E > 0) {
+      const int T = blockDim.x;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (xon[e]) {
+          double acc = 0.0;
+#pragma unroll
+          for (int d = 0; d < LINE_D; ++d) acc = fma(xval[e][d], vec[xidx[e][d]], acc);
+          part[threadIdx.x + e * T] = acc;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int b = 0; b < P; ++b) {
+      double acc = 0.0;
+#pragma unroll
+      for (int d = 0; d < LINE_D; ++d) acc = fma(val[b][d], vec[idx[b][d]], acc);
+      if constexpr (E > 0) {
+        for (int q = pb[b]; q < pb[b] + pn[b]; ++q) acc += part[q];
+      }
+      out[b] = acc;
+    }
+  }
+};
+
 // ------------------------------------------------------------------------
 // PDHG solve kernel: one workgroup per scenario, everything on chip.
+// P = columns and rows owned per thread, E = extra chunk slots per thread.
 // ------------------------------------------------------------------------
-template <int BLOCK, int CPT, int RPT, int MAXD>
+template <int BLOCK, int P, int E>
 __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
+  constexpr int CPT = P, RPT = P;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int s = blockIdx.x;
   const int T = blockDim.x;
   const int tid = threadIdx.x;
-  const int S = a.S, n = a.n, m = a.m, nnz = a.nnz;
-  double *vals = lds;         // [nnz] scaled A~
-  double *xs = vals + nnz;    // [n]   primal trial point x^+ (shared)
-  double *ys = xs + n;        // [m]   dual iterate / dual trial (shared)
-  double *red = ys + m;       // reduction scratch [MAX_WAVES*8]
+  const int S = a.S, n = a.n, m = a.m;
+  double *xs = lds;                 // [n]   primal trial point x^+ (shared)
+  double *ys = xs + n;              // [m]   dual iterate / dual trial (shared)
+  double *part_c = ys + m;          // [xc]  column-chunk partials
+  double *part_r = part_c + a.X.xc; // [xr]  row-chunk partials
+  double *red = part_r + a.X.xr;    // reduction scratch [MAX_WAVES*10]
 
-  const double *vs = a.vals_s + (size_t)s * nnz;
-  for (int k = tid; k < nnz; k += T) vals[k] = vs[k];
-
-  // ---- this thread's matrix entries, cached in VGPRs (index + scaled value)
-  // so each SpMV / SpMV^T step issues only independent LDS loads of the
-  // shared vector; columns/rows longer than MAXD use the pattern loop.
-  int CN[CPT], CB[CPT], CR[CPT][MAXD];
-  double CV[CPT][MAXD];
-  int RN[RPT], RB[RPT], RC[RPT][MAXD];
-  double RV[RPT][MAXD];
+  const double *vs = a.vals_s + (size_t)s * a.nnz;
+  LineRegs<P, E> CL, RW;  // columns (CSC view), rows (CSR view)
 #pragma unroll
-  for (int b = 0; b < CPT; ++b) {
-    int j = tid + b * T;
-    CN[b] = 0;
-    CB[b] = 0;
-    if (j < n) {
-      CB[b] = a.P.col_ptr[j];
-      CN[b] = a.P.col_ptr[j + 1] - CB[b];
-    }
-#pragma unroll
-    for (int e = 0; e < MAXD; ++e) {
-      CR[b][e] = 0;
-      CV[b][e] = 0.0;
-      if (e < CN[b]) {
-        CR[b][e] = a.P.csc_row[CB[b] + e];
-        CV[b][e] = vs[a.P.csc_k[CB[b] + e]];
-      }
-    }
+  for (int b = 0; b < P; ++b) {
+    CL.load_own(b, tid + b * T, n, a.P.col_ptr, a.P.csc_row, a.P.csc_k, vs, a.X.xc ? a.X.c_pb : nullptr);
+    RW.load_own(b, tid + b * T, m, a.P.row_ptr, a.P.col_idx, nullptr, vs, a.X.xr ? a.X.r_pb : nullptr);
   }
 #pragma unroll
-  for (int b = 0; b < RPT; ++b) {
-    int i = tid + b * T;
-    RN[b] = 0;
-    RB[b] = 0;
-    if (i < m) {
-      RB[b] = a.P.row_ptr[i];
-      RN[b] = a.P.row_ptr[i + 1] - RB[b];
-    }
-#pragma unroll
-    for (int e = 0; e < MAXD; ++e) {
-      RC[b][e] = 0;
-      RV[b][e] = 0.0;
-      if (e < RN[b]) {
-        RC[b][e] = a.P.col_idx[RB[b] + e];
-        RV[b][e] = vs[RB[b] + e];
-      }
-    }
+  for (int e = 0; e < (E > 0 ? E : 0); ++e) {
+    CL.load_extra(e, tid + e * T, a.X.xc, a.X.c_pos, a.X.c_len, a.P.csc_row, a.P.csc_k, vs);
+    RW.load_extra(e, tid + e * T, a.X.xr, a.X.r_pos, a.X.r_len, a.P.col_idx, nullptr, vs);
   }
-  // (A^T v)_j for owned column slot b, v in LDS
-  auto coldot = [&](int b, const double *v) -> double {
-    double acc = 0.0;
-    if (CN[b] <= MAXD) {  // padded entries carry value 0 and index 0
-#pragma unroll
-      for (int e = 0; e < MAXD; ++e) acc += CV[b][e] * v[CR[b][e]];
-    } else {
-      for (int p = CB[b]; p < CB[b] + CN[b]; ++p) acc += vals[a.P.csc_k[p]] * v[a.P.csc_row[p]];
-    }
-    return acc;
-  };
-  // (A v)_i for owned row slot b, v in LDS
-  auto rowdot = [&](int b, const double *v) -> double {
-    double acc = 0.0;
-    if (RN[b] <= MAXD) {
-#pragma unroll
-      for (int e = 0; e < MAXD; ++e) acc += RV[b][e] * v[RC[b][e]];
-    } else {
-      for (int p = RB[b]; p < RB[b] + RN[b]; ++p) acc += vals[p] * v[a.P.col_idx[p]];
-    }
-    return acc;
-  };
+  double DOT[P];
 
   // ---- column state in registers
   double X[CPT], Z0X[CPT], G[CPT], Q[CPT], L[CPT], U[CPT], DC[CPT], XN[CPT];
@@ -392,10 +446,11 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     if (i < m) ys[i] = Y[b];
   }
   __syncthreads();
+  RW.dots(xs, part_r, DOT);
 #pragma unroll
   for (int b = 0; b < RPT; ++b) {
     int i = tid + b * T;
-    if (i < m) AX[b] = AZ0[b] = rowdot(b, xs);
+    if (i < m) AX[b] = AZ0[b] = DOT[b];
   }
   __syncthreads();
 
@@ -426,11 +481,12 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     double dxx = 0.0, dyy = 0.0;
 
     // ---- column phase: x+ = clip((x - tau(g - A^T y)) / (1 + tau q))
+    CL.dots(ys, part_c, DOT);
 #pragma unroll
     for (int b = 0; b < CPT; ++b) {
       int j = tid + b * T;
       if (j < n) {
-        const double aty = coldot(b, ys);
+        const double aty = DOT[b];
         double xn = clampd((X[b] - tau * (G[b] - aty)) * IQ[b], L[b], U[b]);
         double d = xn - X[b];
         dxx += d * d;
@@ -441,11 +497,12 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     }
     __syncthreads();
     // ---- row phase: y+ = prox(y - sig A(2x+ - x))
+    RW.dots(xs, part_r, DOT);
 #pragma unroll
     for (int b = 0; b < RPT; ++b) {
       int i = tid + b * T;
       if (i < m) {
-        const double axn = rowdot(b, xs);
+        const double axn = DOT[b];
         double v = Y[b] - sig * (2.0 * axn - AX[b]);
         double yn = fmax(v + sig * RL[b], 0.0) + fmin(v + sig * RU[b], 0.0);
         double d = yn - Y[b];
@@ -475,11 +532,12 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     }
     __syncthreads();
     double pr2 = 0.0, dr2 = 0.0, po = 0.0, dob = 0.0, ddx = 0.0, ddy = 0.0, bl2 = 0.0, g2 = 0.0;
+    CL.dots(ys, part_c, DOT);
 #pragma unroll
     for (int b = 0; b < CPT; ++b) {
       int j = tid + b * T;
       if (j < n) {
-        const double aty = coldot(b, ys);
+        const double aty = DOT[b];
         double lam = (Q[b] * XN[b] + G[b] - aty) / DC[b];  // unscaled reduced cost
         double xu = XN[b] * DC[b];
         double lu = L[b] * DC[b], uu = U[b] * DC[b];
@@ -696,8 +754,12 @@ struct ph_batch {
   double *d_vals_s = nullptr, *d_dr = nullptr, *d_dc = nullptr, *d_eta = nullptr;
   double *d_c = nullptr, *d_l = nullptr, *d_u = nullptr, *d_rl = nullptr, *d_ru = nullptr;
   double *d_diag = nullptr;
+  // extra chunks of lines longer than LINE_D (see LineRegs)
+  int xr = 0, xc = 0;
+  int32_t *d_r_pb = nullptr, *d_r_pos = nullptr, *d_r_len = nullptr;
+  int32_t *d_c_pb = nullptr, *d_c_pos = nullptr, *d_c_len = nullptr;
   bool bound = false;
-  int per = 1, block = 64, maxd = 4;
+  int per = 1, block = 64, ext = 0;
 };
 
 namespace {
@@ -709,35 +771,65 @@ int dalloc(T **p, size_t count) {
   return 0;
 }
 
-// Block size and columns/rows per thread.  Per-thread register state is
-// ~17 doubles per slot, so slots per thread stay <= 6 (VGPR budget at two
-// waves per SIMD); larger scenarios need the streaming kernel (not built).
-bool pick_geometry(int n, int m, int *block, int *per) {
+// Block size, lines (columns and rows) owned per thread and extra-chunk
+// slots per thread.  Per-thread register state is ~30 VGPRs per owned
+// column or row and 12 per extra chunk slot, so slots per thread stay <= 6
+// (VGPR budget at two waves per SIMD); larger scenarios need the streaming
+// kernel (not built).
+bool pick_geometry(int n, int m, int xr, int xc, int *block, int *per, int *ext) {
+  static const int G[][2] = {{64, 1},  {128, 1}, {256, 1}, {256, 2},
+                             {512, 2}, {512, 3}, {512, 4}, {512, 6}};
   const int mx = n > m ? n : m;
-  if (mx <= 64) { *block = 64; *per = 1; }
-  else if (mx <= 128) { *block = 128; *per = 1; }
-  else if (mx <= 256) { *block = 256; *per = 1; }
-  else if (mx <= 512) { *block = 256; *per = 2; }
-  else if (mx <= 1024) { *block = 512; *per = 2; }
-  else if (mx <= 1536) { *block = 512; *per = 3; }
-  else if (mx <= 2048) { *block = 512; *per = 4; }
-  else if (mx <= 3072) { *block = 512; *per = 6; }
-  else return false;
-  return true;
+  const int xx = xr > xc ? xr : xc;
+  for (const auto &g : G) {
+    if (mx > g[0] * g[1]) continue;
+    int e = (xx + g[0] - 1) / g[0];
+    if (e > 4) continue;
+    *block = g[0];
+    *per = g[1];
+    *ext = e == 3 ? 4 : e;
+    return true;
+  }
+  return false;
 }
 
-#define DISPATCH_GEOM(BLK, PER, ...)                                            \
-  do {                                                                          \
-    if (BLK == 64 && PER == 1) { constexpr int B_ = 64, P_ = 1; __VA_ARGS__; }   \
-    else if (BLK == 128 && PER == 1) { constexpr int B_ = 128, P_ = 1; __VA_ARGS__; } \
-    else if (BLK == 256 && PER == 1) { constexpr int B_ = 256, P_ = 1; __VA_ARGS__; } \
-    else if (BLK == 256 && PER == 2) { constexpr int B_ = 256, P_ = 2; __VA_ARGS__; } \
-    else if (BLK == 512 && PER == 2) { constexpr int B_ = 512, P_ = 2; __VA_ARGS__; } \
-    else if (BLK == 512 && PER == 3) { constexpr int B_ = 512, P_ = 3; __VA_ARGS__; } \
-    else if (BLK == 512 && PER == 4) { constexpr int B_ = 512, P_ = 4; __VA_ARGS__; } \
-    else if (BLK == 512 && PER == 6) { constexpr int B_ = 512, P_ = 6; __VA_ARGS__; } \
-    else return fail(PH_EINVAL, "internal: no kernel instance for this geometry"); \
+#define DISPATCH_EXT(BLK, PER, EXT, ...)                                              \
+  do {                                                                               \
+    if (EXT == 0) { constexpr int B_ = BLK, P_ = PER, E_ = 0; __VA_ARGS__; }          \
+    else if (EXT == 1) { constexpr int B_ = BLK, P_ = PER, E_ = 1; __VA_ARGS__; }     \
+    else if (EXT == 2) { constexpr int B_ = BLK, P_ = PER, E_ = 2; __VA_ARGS__; }     \
+    else { constexpr int B_ = BLK, P_ = PER, E_ = 4; __VA_ARGS__; }                   \
   } while (0)
+
+#define DISPATCH_GEOM(BLK, PER, EXT, ...)                                              \
+  do {                                                                                \
+    if (BLK == 64 && PER == 1) DISPATCH_EXT(64, 1, EXT, __VA_ARGS__);                 \
+    else if (BLK == 128 && PER == 1) DISPATCH_EXT(128, 1, EXT, __VA_ARGS__);          \
+    else if (BLK == 256 && PER == 1) DISPATCH_EXT(256, 1, EXT, __VA_ARGS__);          \
+    else if (BLK == 256 && PER == 2) DISPATCH_EXT(256, 2, EXT, __VA_ARGS__);          \
+    else if (BLK == 512 && PER == 2) DISPATCH_EXT(512, 2, EXT, __VA_ARGS__);          \
+    else if (BLK == 512 && PER == 3) DISPATCH_EXT(512, 3, EXT, __VA_ARGS__);          \
+    else if (BLK == 512 && PER == 4) DISPATCH_EXT(512, 4, EXT, __VA_ARGS__);          \
+    else if (BLK == 512 && PER == 6) DISPATCH_EXT(512, 6, EXT, __VA_ARGS__);          \
+    else return fail(PH_EINVAL, "internal: no kernel instance for this geometry");    \
+  } while (0)
+
+// Cut every line (row of the CSR view or column of the CSC view) into its
+// owner's first LINE_D entries plus extra chunks of LINE_D.
+void build_chunks(int lines, const std::vector<int32_t> &ptr, std::vector<int32_t> &pb,
+                  std::vector<int32_t> &pos, std::vector<int32_t> &len) {
+  pb.assign(lines + 1, 0);
+  pos.clear();
+  len.clear();
+  for (int i = 0; i < lines; ++i) {
+    pb[i] = (int32_t)pos.size();
+    for (int p = ptr[i] + LINE_D; p < ptr[i + 1]; p += LINE_D) {
+      pos.push_back(p);
+      len.push_back(std::min(LINE_D, ptr[i + 1] - p));
+    }
+  }
+  pb[lines] = (int32_t)pos.size();
+}
 
 }  // namespace
 
@@ -770,16 +862,16 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
   ph_batch *b = new ph_batch();
   b->S = S; b->n = n; b->m = m; b->nnz = nnz;
   b->stream = (hipStream_t)stream;
-  {  // register-cached entries per row/column: 4 when >= 95% of them fit, else 8
-    int fit4 = 0;
-    for (int i = 0; i < m; ++i) fit4 += (row_ptr[i + 1] - row_ptr[i]) <= 4;
-    for (int j = 0; j < n; ++j) fit4 += (col_ptr[j + 1] - col_ptr[j]) <= 4;
-    b->maxd = (fit4 >= 0.95 * (n + m)) ? 4 : 8;
-  }
-  if (!pick_geometry(n, m, &b->block, &b->per))
-  {
+  std::vector<int32_t> rptr(row_ptr, row_ptr + m + 1);
+  std::vector<int32_t> r_pb, r_pos, r_len, c_pb, c_pos, c_len;
+  build_chunks(m, rptr, r_pb, r_pos, r_len);
+  build_chunks(n, col_ptr, c_pb, c_pos, c_len);
+  b->xr = (int)r_pos.size();
+  b->xc = (int)c_pos.size();
+  if (!pick_geometry(n, m, b->xr, b->xc, &b->block, &b->per, &b->ext)) {
     delete b;
-    return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns; the on-chip PDHG kernel does not cover it");
+    return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns (or too many "
+                           "long rows/columns); the on-chip PDHG kernel does not cover it");
   }
   int rc = 0;
   if ((rc = dalloc(&b->d_row_ptr, m + 1)) || (rc = dalloc(&b->d_col_idx, nnz)) ||
@@ -789,7 +881,10 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_dc, (size_t)S * n)) || (rc = dalloc(&b->d_eta, S)) ||
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
-      (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * 4))) {
+      (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * 4)) ||
+      (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
+      (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
+      (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
     ph_batch_destroy(b);
     return rc;
   }
@@ -803,6 +898,12 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (nnz && cp(b->d_csc_row, csc_row.data(), sizeof(int32_t) * nnz) != hipSuccess) ||
       (nnz && cp(b->d_csc_k, csc_k.data(), sizeof(int32_t) * nnz) != hipSuccess) ||
       cp(b->d_slot_of_col, noslot.data(), sizeof(int32_t) * n) != hipSuccess ||
+      cp(b->d_r_pb, r_pb.data(), sizeof(int32_t) * (m + 1)) != hipSuccess ||
+      cp(b->d_c_pb, c_pb.data(), sizeof(int32_t) * (n + 1)) != hipSuccess ||
+      (b->xr && cp(b->d_r_pos, r_pos.data(), sizeof(int32_t) * b->xr) != hipSuccess) ||
+      (b->xr && cp(b->d_r_len, r_len.data(), sizeof(int32_t) * b->xr) != hipSuccess) ||
+      (b->xc && cp(b->d_c_pos, c_pos.data(), sizeof(int32_t) * b->xc) != hipSuccess) ||
+      (b->xc && cp(b->d_c_len, c_len.data(), sizeof(int32_t) * b->xc) != hipSuccess) ||
       hipStreamSynchronize(b->stream) != hipSuccess) {
     ph_batch_destroy(b);
     return fail(PH_EHIP, "ph_batch_create: copying the pattern failed");
@@ -821,7 +922,7 @@ static size_t scale_lds_bytes(const ph_batch *b) {
   return sizeof(double) * ((size_t)b->nnz + 2 * b->m + 2 * b->n + MAX_WAVES * 8);
 }
 static size_t solve_lds_bytes(const ph_batch *b) {
-  return sizeof(double) * ((size_t)b->nnz + b->n + b->m + MAX_WAVES * 10);
+  return sizeof(double) * ((size_t)b->n + b->m + b->xr + b->xc + MAX_WAVES * 10);
 }
 
 int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const double *l,
@@ -839,7 +940,7 @@ int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const doubl
   const size_t lds = scale_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_batch_bind: scenario does not fit in LDS (nnz+2n+2m too large)");
   Pattern P{b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k};
-  DISPATCH_GEOM(b->block, b->per, {
+  DISPATCH_GEOM(b->block, b->per, 0, {
     hipLaunchKernelGGL((scale_kernel<B_, P_, P_>), dim3(b->S), dim3(B_), lds, b->stream,
                        b->S, b->n, b->m, b->nnz, P, vals, b->d_vals_s, b->d_dr, b->d_dc, b->d_eta);
   });
@@ -878,6 +979,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   SolveArgs a;
   a.S = b->S; a.n = b->n; a.m = b->m; a.nnz = b->nnz;
   a.P = Pattern{b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k};
+  a.X = Chunks{b->xr, b->xc, b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   a.vals_s = b->d_vals_s; a.dr = b->d_dr; a.dc = b->d_dc; a.eta = b->d_eta;
   a.c = b->d_c; a.l = b->d_l; a.u = b->d_u; a.rl = b->d_rl; a.ru = b->d_ru;
   a.slot_of_col = b->d_slot_of_col;
@@ -892,15 +994,9 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
-  if (b->maxd <= 4) {
-    DISPATCH_GEOM(b->block, b->per, {
-      hipLaunchKernelGGL((pdhg_kernel<B_, P_, P_, 4>), dim3(b->S), dim3(B_), lds, b->stream, a);
-    });
-  } else {
-    DISPATCH_GEOM(b->block, b->per, {
-      hipLaunchKernelGGL((pdhg_kernel<B_, P_, P_, 8>), dim3(b->S), dim3(B_), lds, b->stream, a);
-    });
-  }
+  DISPATCH_GEOM(b->block, b->per, b->ext, {
+    hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(b->S), dim3(B_), lds, b->stream, a);
+  });
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -964,7 +1060,8 @@ void ph_batch_destroy(ph_batch_t b) {
   if (!b) return;
   void *ptrs[] = {b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k,
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
-                  b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag};
+                  b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag,
+                  b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete b;
