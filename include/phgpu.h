@@ -45,7 +45,12 @@ typedef struct ph_solve_opts {
   int32_t check_every; /* KKT / restart check period (default 64)           */
   int32_t warm_start;  /* 1: start from x,y,omega passed in (default 1)     */
   double reflection;   /* Halpern reflection gamma in [0,1] (default 1.0)  */
+  int32_t polish;      /* 1: active-set KKT polish for small scenarios     */
+                       /*    (n + m <= 63; default 1)                      */
 } ph_solve_opts;
+
+/* doubles per scenario in ph_batch_get_diag's output */
+#define PH_DIAG_W 5
 
 /* Library version string. */
 const char *ph_version(void);
@@ -155,11 +160,13 @@ int ph_eval_objective(ph_batch_t b, const double *x, const double *W,
                       double prox_on, double *obj);
 
 /*
- * Diagnostics of the last ph_pdhg_solve, copied to host out[4*S]:
+ * Diagnostics of the last ph_pdhg_solve, copied to host out[PH_DIAG_W*S]:
  * per scenario the final relative primal residual, dual residual, duality
- * gap and Halpern fixed-point residual (synchronises the stream).
+ * gap, Halpern fixed-point residual and how the solve ended (0 PDHG reached
+ * tol, 1 active-set polish of the warm start, 2 polish of a PDHG iterate)
+ * (synchronises the stream).
  */
-int ph_batch_get_diag(ph_batch_t b, double *out /*host [S][4]*/);
+int ph_batch_get_diag(ph_batch_t b, double *out /*host [S][PH_DIAG_W]*/);
 
 /* Block until all work queued on the batch's stream has finished. */
 int ph_batch_sync(ph_batch_t b);

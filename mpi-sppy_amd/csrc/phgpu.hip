@@ -231,11 +231,18 @@ struct SolveArgs {
   double *x, *y, *omega;
   int32_t *status, *iters;
   double *pobj, *dbound;
-  double *diag;  // [S][4]: final ep, ed, eg, r (library-owned)
+  double *diag;  // [S][PH_DIAG_W]: final ep, ed, eg, r, how (library-owned)
   double tol;
   int max_iters, check_every, warm;
   double refl;
+  int polish;  // 1: one-wave scenario with n + m <= POLISH_MAX and polish enabled
 };
+
+// Active-set polish: largest KKT system (free columns + active rows) and the
+// KKT error below which a PDHG trial point is polished.
+constexpr int POLISH_MAX = 63;
+constexpr double POLISH_START = 1e-4;
+constexpr int POLISH_ROUNDS = 6;
 
 // Matrix entries a thread keeps in VGPRs for the lines (rows or columns) it
 // owns plus the extra chunks of long lines it helps with.  A line's first
@@ -337,6 +344,7 @@ struct LineRegs {
 template <int BLOCK, int P, int E>
 __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   constexpr int CPT = P, RPT = P;
+  constexpr bool POL = (BLOCK == WAVE && P == 1);  // polish needs lane == line
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int s = blockIdx.x;
   const int T = blockDim.x;
@@ -461,6 +469,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   double out_pobj = 0.0, out_dobj = 0.0;
   double d_ep = -1.0, d_ed = -1.0, d_eg = -1.0, d_r = -1.0;
   const int maxit = a.max_iters;
+  int maxit_eff = maxit;
   const int chk = a.check_every > 0 ? a.check_every : 64;
 
   // step sizes change only with the primal weight: no FP64 division in the
@@ -474,7 +483,271 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   };
   set_steps();
 
-  for (it = 0; it < maxit; ++it) {
+  double LAM[CPT];  // scaled reduced costs of the last KKT evaluation
+  int how = 0;      // 0: PDHG reached tol, 1: polished at start, 2: polished mid-solve
+
+  // Local KKT terms of the trial point (XN, YN, AXN), unscaled; ys must hold
+  // YN.  v[0..5] = primal residual^2, dual residual^2, primal objective,
+  // dual objective, |b|^2, |g|^2.  Contains the column products' barrier.
+  auto kkt_local = [&](double (&v)[10]) {
+    double pr2 = 0.0, dr2 = 0.0, po = 0.0, dob = 0.0, bl2 = 0.0, g2 = 0.0;
+    CL.dots(ys, part_c, DOT);
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) {
+      int j = tid + b * T;
+      LAM[b] = 0.0;
+      if (j < n) {
+        LAM[b] = Q[b] * XN[b] + G[b] - DOT[b];
+        double lam = LAM[b] / DC[b];  // unscaled reduced cost
+        double xu = XN[b] * DC[b];
+        double lu = L[b] * DC[b], uu = U[b] * DC[b];
+        double lp = isfinite(lu) ? fmax(lam, 0.0) : 0.0;
+        double lm = isfinite(uu) ? fmin(lam, 0.0) : 0.0;
+        double rd = lam - lp - lm;
+        dr2 += rd * rd;
+        double qx = Q[b] / (DC[b] * DC[b]);
+        double gu = G[b] / DC[b];
+        po += 0.5 * qx * xu * xu + gu * xu;
+        dob += -0.5 * qx * xu * xu + (lp > 0.0 ? lp * lu : 0.0) + (lm < 0.0 ? lm * uu : 0.0);
+        g2 += gu * gu;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < RPT; ++b) {
+      int i = tid + b * T;
+      if (i < m) {
+        double axu = AXN[b] / DR[b];
+        double rlu = RL[b] / DR[b], ruu = RU[b] / DR[b];
+        double rp = axu - clampd(axu, rlu, ruu);
+        pr2 += rp * rp;
+        double yu = YN[b] * DR[b];
+        dob += (yu > 0.0 ? yu * rlu : 0.0) + (yu < 0.0 ? yu * ruu : 0.0);
+        if (isfinite(rlu)) bl2 += rlu * rlu;
+      }
+    }
+    v[0] = pr2; v[1] = dr2; v[2] = po; v[3] = dob; v[4] = bl2; v[5] = g2;
+  };
+  // relative primal residual, dual residual and gap from block-summed terms;
+  // records the objectives and the diagnostics
+  auto kkt_measures = [&](const double (&v)[10], double &ep, double &ed, double &eg) {
+    ep = sqrt(v[0]) / (1.0 + sqrt(v[4]));
+    ed = sqrt(v[1]) / (1.0 + sqrt(v[5]));
+    const double P0 = v[2] + cst, D0 = v[3] + cst;
+    eg = fabs(P0 - D0) / (1.0 + fabs(P0) + fabs(D0));
+    out_pobj = P0;
+    out_dobj = D0;
+    d_ep = ep; d_ed = ed; d_eg = eg;
+  };
+
+  // Active-set polish (one-wave scenarios, n + m <= POLISH_MAX; lane t owns
+  // column t and row t).  A primal-dual active-set iteration on the exact
+  // KKT system:
+  //  1. classify the trial point: column at a bound when it lies within th
+  //     (relative) of it, row active when its multiplier is nonzero beyond
+  //     th relative to the largest one (|y| > th*max|y|);
+  //  2. solve  q_F x_F - A_RF' y_R = -g_F,  A_RF x_F = b_R - A_R,fixed x_fixed
+  //     by Gauss-Jordan elimination with partial pivoting in LDS (lane =
+  //     matrix column); dependent columns (degenerate duplicate constraints,
+  //     e.g. a row that repeats a variable bound) get the value 0;
+  //  3. accept the clipped point when the full KKT check passes at a.tol,
+  //     else re-classify by the primal-dual active-set rule
+  //       at lower  <=>  lambda + (l - x) > 0,   row at rl <=> y + (rl - Ax) > 0
+  //     and repeat (at most `rounds` solves, stopping on a repeated set).
+  // On success XN/YN/AXN hold the exact point; on failure they are restored.
+  unsigned long long pol_first[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  auto polish_run = [&](double th, int rounds) -> bool {
+    if constexpr (!POL) {
+      return false;
+    } else {
+      const int lane = tid;
+      const double sx = XN[0], sy = YN[0], sa = AXN[0], sl = LAM[0];
+      double *kkt = red + MAX_WAVES * 10;
+      int *cpos = (int *)(kkt + (size_t)(n + m) * (n + m + 1));
+      // ---- 1. initial classification
+      double sc_y = (lane < m) ? fabs(YN[0]) : 0.0;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) sc_y = fmax(sc_y, __shfl_xor(sc_y, off, WAVE));
+      int cs = 0;  // 0 free, 1 at L, 2 at U
+      if (lane < n) {
+        const double xv = XN[0];
+        if (L[0] == U[0]) cs = 1;
+        else if (isfinite(L[0]) && xv - L[0] <= th * (1.0 + fabs(L[0]))) cs = 1;
+        else if (isfinite(U[0]) && U[0] - xv <= th * (1.0 + fabs(U[0]))) cs = 2;
+      }
+      int rs = 0;  // 0 inactive, 1 at rl, 2 at ru
+      if (lane < m) {
+        if (RL[0] == RU[0]) rs = 1;
+        else if (isfinite(RL[0]) && YN[0] > th * sc_y) rs = 1;
+        else if (isfinite(RU[0]) && YN[0] < -th * sc_y) rs = 2;
+      }
+      {
+        const unsigned long long m0 = __ballot(cs == 1), m1 = __ballot(cs == 2);
+        const unsigned long long m2 = __ballot(rs == 1), m3 = __ballot(rs == 2);
+        if (m0 == pol_first[0] && m1 == pol_first[1] && m2 == pol_first[2] && m3 == pol_first[3])
+          return false;  // this starting set was tried already
+        pol_first[0] = m0; pol_first[1] = m1; pol_first[2] = m2; pol_first[3] = m3;
+      }
+      unsigned long long prev[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+      const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      for (int round = 0; round < rounds; ++round) {
+        const unsigned long long m0 = __ballot(cs == 1), m1 = __ballot(cs == 2);
+        const unsigned long long m2 = __ballot(rs == 1), m3 = __ballot(rs == 2);
+        if (m0 == prev[0] && m1 == prev[1] && m2 == prev[2] && m3 == prev[3]) break;  // cycle
+        prev[0] = m0; prev[1] = m1; prev[2] = m2; prev[3] = m3;
+        // ---- 2. KKT system of the active set
+        const bool fr = lane < n && cs == 0;
+        const bool ac = lane < m && rs != 0;
+        const unsigned long long fm = __ballot(fr), am = __ballot(ac);
+        const int nF = __popcll(fm), nR = __popcll(am);
+        const int N = nF + nR, W1 = N + 1;
+        const int pF = __popcll(fm & below), pR = nF + __popcll(am & below);
+        if (lane < n) {
+          cpos[lane] = fr ? pF : -1;
+          xs[lane] = cs == 1 ? L[0] : (cs == 2 ? U[0] : 0.0);
+        }
+        for (int q = lane; q < N * W1; q += WAVE) kkt[q] = 0.0;
+        __syncthreads();
+        if (fr) {
+          kkt[pF * W1 + pF] = Q[0];
+          kkt[pF * W1 + N] = -G[0];
+        }
+        if (ac) {
+          double rhs = rs == 1 ? RL[0] : RU[0];
+          for (int p = a.P.row_ptr[lane]; p < a.P.row_ptr[lane + 1]; ++p) {
+            const int j = a.P.col_idx[p];
+            const double av = vs[p];
+            const int e = cpos[j];
+            if (e >= 0) {
+              kkt[pR * W1 + e] = av;
+              kkt[e * W1 + pR] = -av;
+            } else {
+              rhs -= av * xs[j];
+            }
+          }
+          kkt[pR * W1 + N] = rhs;
+        }
+        __syncthreads();
+        double amax = 0.0;
+        for (int q = lane; q < N * W1; q += WAVE) amax = fmax(amax, fabs(kkt[q]));
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) amax = fmax(amax, __shfl_xor(amax, off, WAVE));
+        const double piv_min = 1e-11 * (amax > 0.0 ? amax : 1.0);
+        int pr = 0, myrow = -1;
+        for (int kk = 0; kk < N && pr < N; ++kk) {
+          double pv = (lane >= pr && lane < N) ? fabs(kkt[lane * W1 + kk]) : -1.0;
+          int pi = lane;
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) {
+            const double ov = __shfl_xor(pv, off, WAVE);
+            const int oi = __shfl_xor(pi, off, WAVE);
+            if (ov > pv || (ov == pv && oi < pi)) {
+              pv = ov;
+              pi = oi;
+            }
+          }
+          if (!(pv > piv_min)) continue;  // dependent column: its unknown stays 0
+          if (pi != pr && lane <= N) {
+            const double t0 = kkt[pr * W1 + lane];
+            kkt[pr * W1 + lane] = kkt[pi * W1 + lane];
+            kkt[pi * W1 + lane] = t0;
+          }
+          __syncthreads();
+          const double piv = kkt[pr * W1 + kk];
+          const double rk = lane <= N ? kkt[pr * W1 + lane] / piv : 0.0;
+          __syncthreads();
+          if (lane <= N) kkt[pr * W1 + lane] = rk;
+          for (int rr = 0; rr < N; ++rr) {
+            if (rr == pr) continue;
+            const double f = kkt[rr * W1 + kk];
+            if (f != 0.0 && lane <= N) kkt[rr * W1 + lane] -= f * rk;
+          }
+          if (lane == kk) myrow = pr;
+          ++pr;
+          __syncthreads();
+        }
+        const double usol = (lane < N && myrow >= 0) ? kkt[myrow * W1 + N] : 0.0;
+        const double uf = __shfl(usol, fr ? pF : 0, WAVE);
+        const double ur = __shfl(usol, ac ? pR : 0, WAVE);
+        double XU = 0.0;
+        if (lane < n) XU = fr ? uf : xs[lane];
+        if (lane < m) YN[0] = ac ? ur : 0.0;
+        // ---- 3. check the clipped point
+        if (lane < n) XN[0] = clampd(XU, L[0], U[0]);
+        __syncthreads();
+        if (lane < n) xs[lane] = XN[0];
+        if (lane < m) ys[lane] = YN[0];
+        __syncthreads();
+        RW.dots(xs, part_r, DOT);
+        if (lane < m) AXN[0] = DOT[0];
+        double v[10];
+        kkt_local(v);
+        v[6] = v[7] = v[8] = v[9] = 0.0;
+        block_sum<10>(v, red);
+        double ep, ed, eg;
+        kkt_measures(v, ep, ed, eg);
+        if (ep <= a.tol && ed <= a.tol && eg <= a.tol) return true;
+        // ---- primal-dual active-set update from the unclipped solution
+        const bool clipped = __ballot(lane < n && XU != XN[0]) != 0ull;
+        double AXU = AXN[0];
+        const double LAMU = LAM[0] + Q[0] * (XU - XN[0]);
+        if (clipped) {
+          __syncthreads();
+          if (lane < n) xs[lane] = XU;
+          __syncthreads();
+          RW.dots(xs, part_r, DOT);
+          AXU = DOT[0];
+        }
+        __syncthreads();
+        if (lane < n) {
+          if (L[0] == U[0]) cs = 1;
+          else if (isfinite(L[0]) && LAMU + (L[0] - XU) > 0.0) cs = 1;
+          else if (isfinite(U[0]) && -LAMU + (XU - U[0]) > 0.0) cs = 2;
+          else cs = 0;
+        }
+        if (lane < m) {
+          if (RL[0] == RU[0]) rs = 1;
+          else if (isfinite(RL[0]) && YN[0] + (RL[0] - AXU) > 0.0) rs = 1;
+          else if (isfinite(RU[0]) && -YN[0] + (AXU - RU[0]) > 0.0) rs = 2;
+          else rs = 0;
+        }
+      }
+      XN[0] = sx;
+      YN[0] = sy;
+      AXN[0] = sa;
+      LAM[0] = sl;
+      __syncthreads();
+      return false;
+    }
+  };
+
+  // warm start: the previous PH iteration's active set usually still holds
+  if constexpr (POL) {
+    if (a.polish && a.warm) {
+#pragma unroll
+      for (int b = 0; b < CPT; ++b) XN[b] = X[b];
+#pragma unroll
+      for (int b = 0; b < RPT; ++b) {
+        YN[b] = Y[b];
+        AXN[b] = AX[b];
+      }
+      bool ok = polish_run(1e-9, POLISH_ROUNDS);
+      if (ok) {
+        stat = PH_STATUS_OPTIMAL;
+        how = 1;
+#pragma unroll
+        for (int b = 0; b < CPT; ++b) X[b] = XN[b];
+#pragma unroll
+        for (int b = 0; b < RPT; ++b) Y[b] = YN[b];
+        maxit_eff = 0;
+      } else {
+        // restore ys <- Y for the iteration
+        if (tid < m) ys[tid] = Y[0];
+        __syncthreads();
+      }
+    }
+  }
+
+  for (it = 0; it < maxit_eff; ++it) {
     const double cb = 1.0 / (double)(k + 2);
     const double ca = (double)(k + 1) * cb;
     const bool check = (it % chk) == 0 || it == maxit - 1;
@@ -531,25 +804,13 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
       if (i < m) ys[i] = YN[b];
     }
     __syncthreads();
-    double pr2 = 0.0, dr2 = 0.0, po = 0.0, dob = 0.0, ddx = 0.0, ddy = 0.0, bl2 = 0.0, g2 = 0.0;
-    CL.dots(ys, part_c, DOT);
+    double v[10];
+    kkt_local(v);
+    double ddx = 0.0, ddy = 0.0;
 #pragma unroll
     for (int b = 0; b < CPT; ++b) {
       int j = tid + b * T;
       if (j < n) {
-        const double aty = DOT[b];
-        double lam = (Q[b] * XN[b] + G[b] - aty) / DC[b];  // unscaled reduced cost
-        double xu = XN[b] * DC[b];
-        double lu = L[b] * DC[b], uu = U[b] * DC[b];
-        double lp = isfinite(lu) ? fmax(lam, 0.0) : 0.0;
-        double lm = isfinite(uu) ? fmin(lam, 0.0) : 0.0;
-        double rd = lam - lp - lm;
-        dr2 += rd * rd;
-        double qx = Q[b] / (DC[b] * DC[b]);
-        double gu = G[b] / DC[b];
-        po += 0.5 * qx * xu * xu + gu * xu;
-        dob += -0.5 * qx * xu * xu + (lp > 0.0 ? lp * lu : 0.0) + (lm < 0.0 ? lm * uu : 0.0);
-        g2 += gu * gu;
         double e = XN[b] - Z0X[b];
         ddx += e * e;
       }
@@ -558,27 +819,19 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     for (int b = 0; b < RPT; ++b) {
       int i = tid + b * T;
       if (i < m) {
-        double axu = AXN[b] / DR[b];
-        double rlu = RL[b] / DR[b], ruu = RU[b] / DR[b];
-        double rp = axu - clampd(axu, rlu, ruu);
-        pr2 += rp * rp;
-        double yu = YN[b] * DR[b];
-        dob += (yu > 0.0 ? yu * rlu : 0.0) + (yu < 0.0 ? yu * ruu : 0.0);
-        if (isfinite(rlu)) bl2 += rlu * rlu;
         double e = YN[b] - Z0Y[b];
         ddy += e * e;
       }
     }
-    double v[10] = {pr2, dr2, po, dob, ddx, ddy, bl2, g2, dxx, dyy};
+    v[6] = ddx;
+    v[7] = ddy;
+    v[8] = dxx;
+    v[9] = dyy;
     block_sum<10>(v, red);
-    const double ep = sqrt(v[0]) / (1.0 + sqrt(v[6]));
-    const double ed = sqrt(v[1]) / (1.0 + sqrt(v[7]));
-    const double P0 = v[2] + cst, D0 = v[3] + cst;
-    const double eg = fabs(P0 - D0) / (1.0 + fabs(P0) + fabs(D0));
-    out_pobj = P0;
-    out_dobj = D0;
+    double ep, ed, eg;
+    kkt_measures(v, ep, ed, eg);
     const double r = sqrt(omega * v[8] + v[9] / omega);
-    d_ep = ep; d_ed = ed; d_eg = eg; d_r = r;
+    d_r = r;
     if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
       stat = PH_STATUS_OPTIMAL;
 #pragma unroll
@@ -587,6 +840,24 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
       for (int b = 0; b < RPT; ++b) Y[b] = YN[b];
       ++it;
       break;
+    }
+    if constexpr (POL) {
+      // near the optimum: guess the active set from the trial point and
+      // solve its KKT system; accepted only if the KKT check passes
+      const double err = fmax(ep, fmax(ed, eg));
+      if (a.polish && err <= POLISH_START) {
+        bool ok = polish_run(fmin(sqrt(err), 1e-3), POLISH_ROUNDS);
+        if (ok) {
+          stat = PH_STATUS_OPTIMAL;
+          how = 2;
+#pragma unroll
+          for (int b = 0; b < CPT; ++b) X[b] = XN[b];
+#pragma unroll
+          for (int b = 0; b < RPT; ++b) Y[b] = YN[b];
+          ++it;
+          break;
+        }
+      }
     }
     bool restart = false;
     if (r_restart < 0.0) {
@@ -606,7 +877,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
       restart = true;
     } else if (restart) {
       // PDLP primal weight update, smoothing 0.5
-      const double dx = sqrt(v[4]), dy = sqrt(v[5]);
+      const double dx = sqrt(v[6]), dy = sqrt(v[7]);
       if (dx > 1e-12 && dy > 1e-12) omega = exp(0.5 * log(dy / dx) + 0.5 * log(omega));
     }
     if (restart) {
@@ -647,10 +918,11 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     a.iters[s] = it;
     a.pobj[s] = out_pobj;
     a.dbound[s] = out_dobj;
-    a.diag[4 * s + 0] = d_ep;
-    a.diag[4 * s + 1] = d_ed;
-    a.diag[4 * s + 2] = d_eg;
-    a.diag[4 * s + 3] = d_r;
+    a.diag[PH_DIAG_W * s + 0] = d_ep;
+    a.diag[PH_DIAG_W * s + 1] = d_ed;
+    a.diag[PH_DIAG_W * s + 2] = d_eg;
+    a.diag[PH_DIAG_W * s + 3] = d_r;
+    a.diag[PH_DIAG_W * s + 4] = (double)how;
   }
 }
 
@@ -795,10 +1067,10 @@ bool pick_geometry(int n, int m, int xr, int xc, int *block, int *per, int *ext)
 
 #define DISPATCH_EXT(BLK, PER, EXT, ...)                                              \
   do {                                                                               \
-    if (EXT == 0) { constexpr int B_ = BLK, P_ = PER, E_ = 0; __VA_ARGS__; }          \
-    else if (EXT == 1) { constexpr int B_ = BLK, P_ = PER, E_ = 1; __VA_ARGS__; }     \
-    else if (EXT == 2) { constexpr int B_ = BLK, P_ = PER, E_ = 2; __VA_ARGS__; }     \
-    else { constexpr int B_ = BLK, P_ = PER, E_ = 4; __VA_ARGS__; }                   \
+    if (EXT == 0) { constexpr int B_ = BLK, P_ = PER, E_ = 0; (void)E_; __VA_ARGS__; }          \
+    else if (EXT == 1) { constexpr int B_ = BLK, P_ = PER, E_ = 1; (void)E_; __VA_ARGS__; }     \
+    else if (EXT == 2) { constexpr int B_ = BLK, P_ = PER, E_ = 2; (void)E_; __VA_ARGS__; }     \
+    else { constexpr int B_ = BLK, P_ = PER, E_ = 4; (void)E_; __VA_ARGS__; }                   \
   } while (0)
 
 #define DISPATCH_GEOM(BLK, PER, EXT, ...)                                              \
@@ -881,7 +1153,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_dc, (size_t)S * n)) || (rc = dalloc(&b->d_eta, S)) ||
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
-      (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * 4)) ||
+      (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
       (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
@@ -921,8 +1193,17 @@ int ph_batch_set_stream(ph_batch_t b, void *stream) {
 static size_t scale_lds_bytes(const ph_batch *b) {
   return sizeof(double) * ((size_t)b->nnz + 2 * b->m + 2 * b->n + MAX_WAVES * 8);
 }
+static bool polish_fits(const ph_batch *b) {
+  return b->block == WAVE && b->per == 1 && b->n + b->m <= POLISH_MAX;
+}
 static size_t solve_lds_bytes(const ph_batch *b) {
-  return sizeof(double) * ((size_t)b->n + b->m + b->xr + b->xc + MAX_WAVES * 10);
+  size_t d = (size_t)b->n + b->m + b->xr + b->xc + MAX_WAVES * 10;
+  size_t extra = 0;
+  if (polish_fits(b)) {  // KKT matrix + free-column positions
+    const size_t N = (size_t)b->n + b->m;
+    extra = sizeof(double) * N * (N + 1) + sizeof(int32_t) * b->n;
+  }
+  return sizeof(double) * d + extra;
 }
 
 int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const double *l,
@@ -991,6 +1272,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.check_every = opts ? opts->check_every : 64;
   a.warm = opts ? opts->warm_start : 1;
   a.refl = opts ? opts->reflection : 1.0;
+  a.polish = (opts ? opts->polish : 1) && polish_fits(b);
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
@@ -1045,7 +1327,7 @@ int ph_eval_objective(ph_batch_t b, const double *x, const double *W, const doub
 
 int ph_batch_get_diag(ph_batch_t b, double *out) {
   if (!b || !out) return fail(PH_EINVAL, "ph_batch_get_diag: bad arguments");
-  HIP_OK(hipMemcpyAsync(out, b->d_diag, sizeof(double) * 4 * (size_t)b->S, hipMemcpyDeviceToHost, b->stream));
+  HIP_OK(hipMemcpyAsync(out, b->d_diag, sizeof(double) * PH_DIAG_W * (size_t)b->S, hipMemcpyDeviceToHost, b->stream));
   HIP_OK(hipStreamSynchronize(b->stream));
   return PH_OK;
 }

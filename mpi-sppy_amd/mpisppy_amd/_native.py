@@ -23,7 +23,10 @@ class PHGPUError(RuntimeError):
 
 class SolveOpts(ctypes.Structure):
     _fields_ = [("tol", _c_dbl), ("max_iters", _c_int), ("check_every", _c_int),
-                ("warm_start", _c_int), ("reflection", _c_dbl)]
+                ("warm_start", _c_int), ("reflection", _c_dbl), ("polish", _c_int)]
+
+
+DIAG_W = 5  # PH_DIAG_W in include/phgpu.h
 
 
 # (name, restype, argtypes) -- must match include/phgpu.h exactly

@@ -187,9 +187,9 @@ class DeviceBatch:
         self.const = up(data.const)
 
     def solve(self, W, rho, xbar, w_on, prox_on, tol=1e-9, max_iters=200000,
-              check_every=64, warm_start=True, reflection=1.0):
+              check_every=64, warm_start=True, reflection=1.0, polish=True):
         opts = _native.SolveOpts(float(tol), int(max_iters), int(check_every),
-                                 1 if warm_start else 0, float(reflection))
+                                 1 if warm_start else 0, float(reflection), 1 if polish else 0)
         _native.check(self.lib.ph_pdhg_solve(
             self.handle, _native.ptr(W), _native.ptr(rho), _native.ptr(xbar),
             float(w_on), float(prox_on), _native.ptr(self.x), _native.ptr(self.y),
@@ -219,8 +219,9 @@ class DeviceBatch:
                                                  float(prox_on), _native.ptr(out)), "ph_eval_objective")
 
     def diagnostics(self):
-        """[S][4] host array: final (primal res, dual res, gap, fixed-point res)."""
-        out = np.zeros((self.S, 4))
+        """[S][5] host array: final (primal res, dual res, gap, fixed-point res,
+        how: 0 PDHG tol, 1 warm-start polish, 2 polish of a PDHG iterate)."""
+        out = np.zeros((self.S, _native.DIAG_W))
         _native.check(self.lib.ph_batch_get_diag(self.handle, out.ctypes.data_as(_native._c_ptr)),
                       "ph_batch_get_diag")
         return out

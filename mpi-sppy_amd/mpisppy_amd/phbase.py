@@ -24,9 +24,9 @@ from .spbase import SPBase
 # solver option keys understood by the PDHG batch (iter0/iterk_solver_options)
 _PDHG_KEYS = {"pdhg_tol": "tol", "pdhg_max_iters": "max_iters",
               "pdhg_check_every": "check_every", "warm_start": "warm_start",
-              "pdhg_reflection": "reflection"}
+              "pdhg_reflection": "reflection", "pdhg_polish": "polish"}
 _DEFAULT_SOLVE = dict(tol=1e-9, max_iters=200000, check_every=64, warm_start=True,
-                      reflection=1.0)
+                      reflection=1.0, polish=True)
 
 
 class PHBase(SPBase):
