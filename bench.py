@@ -41,6 +41,16 @@ def bytes_per_pdhg_iter(c):
     return 8 * (2 * nnz + 7 * n + 5 * m)
 
 
+def solve_bytes_per_scenario(c):
+    """HBM bytes one scenario solve must move at least: scaled matrix values
+    (nnz), row/column scalings (m+n), c/l/u (3n), rl/ru (2m), the x/y warm
+    start in and the solution out (2n+2m), W/rho/xbar (3K), step size,
+    primal weight in/out, status/iters, pobj/dbound and diagnostics (13)."""
+    n, m, nnz = farmer_dims(c)
+    K = 3 * c
+    return 8 * (nnz + (n + m) + 3 * n + 2 * m + 2 * (n + m) + 3 * K + 13)
+
+
 def cpu_baseline(c, sample_scens, min_seconds=10.0):
     """Oracle subproblem engine (HiGHS 1.8 from scipy) timed on this host,
     one core, on a bounded sample of the same workload: the prox-QPs of one
@@ -138,43 +148,40 @@ def run():
     for _ in range(args.warmup):
         ph_iteration()
     b = ph.batch
-    stream = torch.cuda.current_stream()
-    ev = []
-    it_counts = []
+    b.time_kernel = True  # HIP events around each solve launch, on the batch's stream
+    kern_ms = []
     ph.solve_log.clear()
-    # timed region
+    # timed region: exactly the reference's iterk_loop body (phbase.py:1498-1553)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ph.Compute_Xbar(False)
-        ph.Update_W(False)
-        ph.conv = ph.convergence_diff()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        b.solve(ph.W, ph.rho, ph.xbar, ph.w_on, ph.prox_on)
-        e1.record(stream)
-        ev.append((e0, e1))
-        it_counts.append(b.iters.sum())  # device scalar, read after the region
+        ph_iteration()
+        kern_ms.append(b.kernel_ms())  # the solve has completed (solve_loop synchronised)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt_local = time.perf_counter() - t0
+    b.time_kernel = False
     dts = torch.tensor([dt_local], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(dts, op=dist.ReduceOp.MAX)
     dt = float(dts.item())
 
-    kern_ms = [a.elapsed_time(z) for a, z in ev]
-    tot_iters = float(sum(int(x.item()) for x in it_counts))
     S_loc = ph.S_loc
-    kern_s = sum(kern_ms) / 1000.0
+    log = ph.solve_log[-args.steps:]
+    tot_iters = float(sum(x[2] * x[0] for x in log))
+    n_polished = float(sum(x[4] for x in log))
     mean_kernel_ms = float(np.mean(kern_ms))
-    alg_bytes_per_launch = tot_iters / len(kern_ms) * bytes_per_pdhg_iter(c)
+    # algorithmic HBM bytes per launch: every scenario's data in and its
+    # solution out once (solve_bytes_per_scenario) + the PDHG fallback steps
+    # that do not fit on chip in a streaming design (bytes_per_pdhg_iter each)
+    alg_bytes_per_launch = (S_loc * solve_bytes_per_scenario(c)
+                            + tot_iters / len(kern_ms) * bytes_per_pdhg_iter(c))
     achieved_gbs = alg_bytes_per_launch / (mean_kernel_ms / 1000.0) / 1e9
     mean_iters = tot_iters / len(kern_ms) / S_loc
+    polished_frac = n_polished / len(kern_ms) / S_loc
 
     # PH wall-clock to convergence tolerance (fresh run, same instance)
     tol_info = None
@@ -239,10 +246,12 @@ def run():
                          "kernel": "pdhg_kernel",
                          "kernel_ms": round(mean_kernel_ms, 4),
                          "alg_bytes_per_launch": alg_bytes_per_launch,
-                         "note": "algorithmic bytes = SURVEY 8(d) B_it per scenario-PDHG-iteration "
-                                 "x PDHG iterations in the launch; the kernel keeps each scenario "
-                                 "on chip (LDS+VGPR), so HBM traffic is far below this"},
-            "pdhg_iters_per_solve": round(mean_iters, 1),
+                         "note": "algorithmic bytes per launch = S x the scenario's data in and "
+                                 "solution out (solve_bytes_per_scenario) + SURVEY 8(d) B_it x the "
+                                 "PDHG fallback steps taken; warm solves finish by the on-chip "
+                                 "active-set KKT solve, so the kernel is latency-bound, not HBM-bound"},
+            "pdhg_iters_per_solve": round(mean_iters, 2),
+            "polished_fraction": round(polished_frac, 4),
             "ph_to_tol": tol_info,
             "cpu_baseline": cpu,
         }

@@ -168,6 +168,16 @@ int ph_eval_objective(ph_batch_t b, const double *x, const double *W,
  */
 int ph_batch_get_diag(ph_batch_t b, double *out /*host [S][PH_DIAG_W]*/);
 
+/*
+ * Summary of the last ph_pdhg_solve, copied to host (synchronises the
+ * stream): out[0] scenarios not solved to tolerance (status != optimal),
+ * out[1] PDHG iterations summed over scenarios, out[2] the largest count,
+ * out[3] scenarios finished by the active-set polish.  One small copy
+ * replaces reading status[S] after every solve (phbase.py:959-965 checks
+ * each scenario's status).
+ */
+int ph_batch_solve_summary(ph_batch_t b, int64_t *out /*host [4]*/);
+
 /* Block until all work queued on the batch's stream has finished. */
 int ph_batch_sync(ph_batch_t b);
 

@@ -232,6 +232,7 @@ struct SolveArgs {
   int32_t *status, *iters;
   double *pobj, *dbound;
   double *diag;  // [S][PH_DIAG_W]: final ep, ed, eg, r, how (library-owned)
+  unsigned long long *summary;  // [4]: not optimal, sum iters, max iters, polished
   double tol;
   int max_iters, check_every, warm;
   double refl;
@@ -923,6 +924,10 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     a.diag[PH_DIAG_W * s + 2] = d_eg;
     a.diag[PH_DIAG_W * s + 3] = d_r;
     a.diag[PH_DIAG_W * s + 4] = (double)how;
+    if (stat != PH_STATUS_OPTIMAL) atomicAdd(&a.summary[0], 1ull);
+    atomicAdd(&a.summary[1], (unsigned long long)it);
+    atomicMax(&a.summary[2], (unsigned long long)it);
+    if (how) atomicAdd(&a.summary[3], 1ull);
   }
 }
 
@@ -1026,6 +1031,7 @@ struct ph_batch {
   double *d_vals_s = nullptr, *d_dr = nullptr, *d_dc = nullptr, *d_eta = nullptr;
   double *d_c = nullptr, *d_l = nullptr, *d_u = nullptr, *d_rl = nullptr, *d_ru = nullptr;
   double *d_diag = nullptr;
+  unsigned long long *d_summary = nullptr;
   // extra chunks of lines longer than LINE_D (see LineRegs)
   int xr = 0, xc = 0;
   int32_t *d_r_pb = nullptr, *d_r_pos = nullptr, *d_r_len = nullptr;
@@ -1154,6 +1160,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
       (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
+      (rc = dalloc(&b->d_summary, 4)) ||
       (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
@@ -1266,7 +1273,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.slot_of_col = b->d_slot_of_col;
   a.W = W; a.rho = rho; a.xbar = xbar; a.w_on = w_on; a.prox_on = prox_on;
   a.x = x; a.y = y; a.omega = omega; a.status = status; a.iters = iters;
-  a.pobj = pobj; a.dbound = dbound; a.diag = b->d_diag;
+  a.pobj = pobj; a.dbound = dbound; a.diag = b->d_diag; a.summary = b->d_summary;
   a.tol = opts ? opts->tol : 1e-9;
   a.max_iters = opts ? opts->max_iters : 200000;
   a.check_every = opts ? opts->check_every : 64;
@@ -1276,6 +1283,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
+  HIP_OK(hipMemsetAsync(b->d_summary, 0, 4 * sizeof(unsigned long long), b->stream));
   DISPATCH_GEOM(b->block, b->per, b->ext, {
     hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(b->S), dim3(B_), lds, b->stream, a);
   });
@@ -1332,6 +1340,15 @@ int ph_batch_get_diag(ph_batch_t b, double *out) {
   return PH_OK;
 }
 
+int ph_batch_solve_summary(ph_batch_t b, int64_t *out) {
+  if (!b || !out) return fail(PH_EINVAL, "ph_batch_solve_summary: bad arguments");
+  unsigned long long h[4];
+  HIP_OK(hipMemcpyAsync(h, b->d_summary, sizeof(h), hipMemcpyDeviceToHost, b->stream));
+  HIP_OK(hipStreamSynchronize(b->stream));
+  for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
+  return PH_OK;
+}
+
 int ph_batch_sync(ph_batch_t b) {
   if (!b) return fail(PH_EINVAL, "null batch");
   HIP_OK(hipStreamSynchronize(b->stream));
@@ -1342,7 +1359,7 @@ void ph_batch_destroy(ph_batch_t b) {
   if (!b) return;
   void *ptrs[] = {b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k,
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
-                  b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag,
+                  b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

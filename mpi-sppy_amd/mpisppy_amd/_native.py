@@ -47,6 +47,7 @@ SIGNATURES = [
     ("ph_segment_sum", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_int, _c_ptr, _c_ptr]),
     ("ph_eval_objective", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_dbl, _c_dbl, _c_ptr]),
     ("ph_batch_get_diag", _c_int, [_c_ptr, _c_ptr]),
+    ("ph_batch_solve_summary", _c_int, [_c_ptr, _c_ptr]),
     ("ph_batch_sync", _c_int, [_c_ptr]),
     ("ph_batch_destroy", None, [_c_ptr]),
 ]

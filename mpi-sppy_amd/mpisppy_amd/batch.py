@@ -185,16 +185,38 @@ class DeviceBatch:
         self.pobj = torch.zeros(self.S, **f64)
         self.dbound = torch.zeros(self.S, **f64)
         self.const = up(data.const)
+        self._summary = np.zeros(4, dtype=np.int64)
+        self.time_kernel = False  # record HIP events around each solve launch
+        self._events = None
 
     def solve(self, W, rho, xbar, w_on, prox_on, tol=1e-9, max_iters=200000,
               check_every=64, warm_start=True, reflection=1.0, polish=True):
         opts = _native.SolveOpts(float(tol), int(max_iters), int(check_every),
                                  1 if warm_start else 0, float(reflection), 1 if polish else 0)
+        if self.time_kernel:
+            stream = torch.cuda.current_stream(self.dev) if self.stream is None else self.stream
+            self._events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self._events[0].record(stream)
         _native.check(self.lib.ph_pdhg_solve(
             self.handle, _native.ptr(W), _native.ptr(rho), _native.ptr(xbar),
             float(w_on), float(prox_on), _native.ptr(self.x), _native.ptr(self.y),
             _native.ptr(self.omega), _native.ptr(self.status), _native.ptr(self.iters),
             _native.ptr(self.pobj), _native.ptr(self.dbound), opts), "ph_pdhg_solve")
+        if self.time_kernel:
+            self._events[1].record(stream)
+
+    def kernel_ms(self):
+        """Duration of the last solve launch (HIP events on the batch's stream)."""
+        if self._events is None:
+            return None
+        return self._events[0].elapsed_time(self._events[1])
+
+    def summary(self):
+        """(not optimal, sum of PDHG iterations, max iterations, polished) of the
+        last solve; synchronises the stream (one 32-byte copy)."""
+        _native.check(self.lib.ph_batch_solve_summary(
+            self.handle, self._summary.ctypes.data_as(_native._c_ptr)), "ph_batch_solve_summary")
+        return tuple(int(v) for v in self._summary)
 
     def xbar_accum(self, prob_coeff, slot_k, slot_s0, slot_s1, out):
         G = slot_k.numel()

@@ -65,7 +65,7 @@ class PHBase(SPBase):
         self.device = torch.device("cuda", torch.cuda.current_device()) \
             if torch.cuda.is_available() else torch.device("cpu")
         self._warned_keys = set()
-        self.solve_log = []   # (n_scenarios, seconds, mean iters, max iters)
+        self.solve_log = []   # (n_scenarios, seconds, mean iters, max iters, polished)
         self._alloc_state()
         self.attach_xbars()
         if self.PH_extensions is not None:
@@ -110,6 +110,7 @@ class PHBase(SPBase):
         self.conv_cnt = np.array([max(len(sl), 1) * K for sl in slices], dtype=np.float64)
         self.conv_parts = torch.zeros(R, **f64)
         self.scenario_feasible = np.ones(S, dtype=bool)
+        self._all_feasible = True
 
     # ---------------------------------------------------------- options --
     def options_check(self):
@@ -227,16 +228,20 @@ class PHBase(SPBase):
             self._create_solvers()
         kw = self._solve_kwargs(solver_options)
         b = self.batch
-        self._sync()
         t0 = time.perf_counter()
         b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
-        self._sync()
+        nonopt, it_sum, it_max, npol = b.summary()  # waits for the solve
         dt = time.perf_counter() - t0
-        status = b.status.cpu().numpy()
-        iters = b.iters.cpu().numpy()
-        self.solve_log.append((self.S_loc, dt, float(iters.mean()), int(iters.max())))
-        self.scenario_feasible = (status == 0) | (status == 1)
-        nlim = int(np.sum(status == 1))
+        self.solve_log.append((self.S_loc, dt, it_sum / max(self.S_loc, 1), it_max, npol))
+        if nonopt:
+            status = b.status.cpu().numpy()
+            self.scenario_feasible = (status == 0) | (status == 1)
+            nlim = int(np.sum(status == 1))
+        else:
+            if not self._all_feasible:
+                self.scenario_feasible = np.ones(self.S_loc, dtype=bool)
+            nlim = 0
+        self._all_feasible = not nonopt
         if nlim and gripe:
             print(f"[{type(self).__name__}] {nlim} scenario(s) stopped at the PDHG "
                   f"iteration limit ({kw['max_iters']})")

@@ -1,6 +1,6 @@
 """Test-only stand-in for DeviceBatch on CPU tensors.
 
-Implements the five device operations PHBase calls (solve, xbar_accum,
+Implements the device operations PHBase calls (solve, summary, xbar_accum,
 update_w, segment_sum, eval_objective) with torch CPU ops and the oracle's
 exact per-scenario solver, so the distributed *host* logic of PHBase
 (slicing, node slots, allreduces, convergence bookkeeping) can be tested
@@ -47,6 +47,11 @@ class CPUBatch:
             self.pobj[s] = v
             self.dbound[s] = v
             self.status[s] = 0
+
+    def summary(self):
+        st = self.status.numpy()
+        it = self.iters.numpy()
+        return int(np.sum(st != 0)), int(it.sum()), int(it.max(initial=0)), 0
 
     def xbar_accum(self, prob_coeff, slot_k, slot_s0, slot_s1, out):
         X = self.x.view(self.n, self.S)[self.cols]
