@@ -232,11 +232,16 @@ struct SolveArgs {
   int32_t *status, *iters;
   double *pobj, *dbound;
   double *diag;  // [S][PH_DIAG_W]: final ep, ed, eg, r, how (library-owned)
-  unsigned long long *summary;  // [4]: not optimal, sum iters, max iters, polished
   double tol;
   int max_iters, check_every, warm;
   double refl;
   int polish;  // 1: one-wave scenario with n + m <= POLISH_MAX and polish enabled
+  // active-set cache (see CacheArgs); cache == null: no caching
+  int K, CW;
+  const int32_t *nonant_col;
+  double *cache;
+  int32_t *cache_ok;
+  const int32_t *done;  // [S] or null: 1 = solved by active_set_kernel, skip
 };
 
 // Active-set polish: largest KKT system (free columns + active rows) and the
@@ -339,6 +344,307 @@ struct LineRegs {
 };
 
 // ------------------------------------------------------------------------
+// KKT check of a trial point, in the unscaled space.  Per-line terms are
+// accumulated into v[0..5] = primal residual^2, dual residual^2, primal
+// objective, dual objective, |b|^2, |g|^2 and block-summed by the caller.
+// (Scaled: x = XN*DC, reduced cost = (Q XN + G - A~'y)/DC, A x = AXN/DR,
+// y = YN*DR.)  Sign convention: y > 0 <=> row at rl, lambda > 0 <=> at l.
+// ------------------------------------------------------------------------
+template <int NV>
+__device__ __forceinline__ void kkt_terms_col(double XN, double G, double Q, double L, double U,
+                                              double DC, double aty, double &lam_s,
+                                              double (&v)[NV]) {
+  lam_s = Q * XN + G - aty;
+  const double lam = lam_s / DC;  // unscaled reduced cost
+  const double xu = XN * DC;
+  const double lu = L * DC, uu = U * DC;
+  const double lp = isfinite(lu) ? fmax(lam, 0.0) : 0.0;
+  const double lm = isfinite(uu) ? fmin(lam, 0.0) : 0.0;
+  const double rd = lam - lp - lm;
+  const double qx = Q / (DC * DC);
+  const double gu = G / DC;
+  v[1] += rd * rd;
+  v[2] += 0.5 * qx * xu * xu + gu * xu;
+  v[3] += -0.5 * qx * xu * xu + (lp > 0.0 ? lp * lu : 0.0) + (lm < 0.0 ? lm * uu : 0.0);
+  v[5] += gu * gu;
+}
+
+template <int NV>
+__device__ __forceinline__ void kkt_terms_row(double AXN, double YN, double RL, double RU,
+                                              double DR, double (&v)[NV]) {
+  const double axu = AXN / DR;
+  const double rlu = RL / DR, ruu = RU / DR;
+  const double rp = axu - clampd(axu, rlu, ruu);
+  const double yu = YN * DR;
+  v[0] += rp * rp;
+  v[3] += (yu > 0.0 ? yu * rlu : 0.0) + (yu < 0.0 ? yu * ruu : 0.0);
+  if (isfinite(rlu)) v[4] += rlu * rlu;
+}
+
+template <int NV>
+__device__ __forceinline__ void kkt_rel(const double (&v)[NV], double cst, double &ep, double &ed,
+                                        double &eg, double &pobj, double &dobj) {
+  ep = sqrt(v[0]) / (1.0 + sqrt(v[4]));
+  ed = sqrt(v[1]) / (1.0 + sqrt(v[5]));
+  pobj = v[2] + cst;
+  dobj = v[3] + cst;
+  eg = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
+}
+
+// ------------------------------------------------------------------------
+// Active-set KKT machinery (one wave per scenario, lane t owns column t and
+// row t; n + m <= POLISH_MAX).  A primal-dual active-set iteration on the
+// exact KKT system of the scaled subproblem:
+//  1. classify a trial point: column at a bound when it lies within th
+//     (relative) of it, row active when its multiplier is nonzero beyond th
+//     relative to the largest one (|y| > th*max|y|);
+//  2. solve  q_F x_F - A_RF' y_R = -g_F,  A_RF x_F = b_R - A_R,fixed x_fixed
+//     by Gauss-Jordan elimination with partial pivoting in LDS (lane =
+//     matrix column); dependent columns (degenerate duplicate constraints,
+//     e.g. a row that repeats a variable bound) get the value 0;
+//  3. accept the clipped point when the full KKT check passes at tol, else
+//     re-classify by the primal-dual active-set rule
+//       at lower <=> lambda + (l - x) > 0,   row at rl <=> y + (rl - Ax) > 0
+//     and repeat (at most POLISH_ROUNDS solves, stopping on a repeated set).
+// ------------------------------------------------------------------------
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, WAVE));
+  return v;
+}
+
+struct ActiveSet {
+  int cs;  // column: 0 free, 1 at L, 2 at U
+  int rs;  // row: 0 inactive, 1 at rl, 2 at ru
+  __device__ __forceinline__ void signature(unsigned long long (&sig)[4]) const {
+    sig[0] = __ballot(cs == 1);
+    sig[1] = __ballot(cs == 2);
+    sig[2] = __ballot(rs == 1);
+    sig[3] = __ballot(rs == 2);
+  }
+};
+
+__device__ __forceinline__ bool same_sig(const unsigned long long (&a)[4],
+                                         const unsigned long long (&b)[4]) {
+  return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3];
+}
+
+// step 1: columns by distance to the bound, rows by multiplier sign
+__device__ __forceinline__ ActiveSet classify_trial(int lane, int n, int m, double th, double x,
+                                                    double y, double L, double U, double RL,
+                                                    double RU) {
+  const double sc_y = wave_max(lane < m ? fabs(y) : 0.0);
+  ActiveSet as{0, 0};
+  if (lane < n) {
+    if (L == U) as.cs = 1;
+    else if (isfinite(L) && x - L <= th * (1.0 + fabs(L))) as.cs = 1;
+    else if (isfinite(U) && U - x <= th * (1.0 + fabs(U))) as.cs = 2;
+  }
+  if (lane < m) {
+    if (RL == RU) as.rs = 1;
+    else if (isfinite(RL) && y > th * sc_y) as.rs = 1;
+    else if (isfinite(RU) && y < -th * sc_y) as.rs = 2;
+  }
+  return as;
+}
+
+// step 3: primal-dual active-set rule from the unclipped solution
+__device__ __forceinline__ ActiveSet classify_pdas(int lane, int n, int m, double xu, double lamu,
+                                                   double y, double axu, double L, double U,
+                                                   double RL, double RU) {
+  ActiveSet as{0, 0};
+  if (lane < n) {
+    if (L == U) as.cs = 1;
+    else if (isfinite(L) && lamu + (L - xu) > 0.0) as.cs = 1;
+    else if (isfinite(U) && -lamu + (xu - U) > 0.0) as.cs = 2;
+  }
+  if (lane < m) {
+    if (RL == RU) as.rs = 1;
+    else if (isfinite(RL) && y + (RL - axu) > 0.0) as.rs = 1;
+    else if (isfinite(RU) && -y + (axu - RU) > 0.0) as.rs = 2;
+  }
+  return as;
+}
+
+// Result of active_set_solve: the unclipped column value xu (fixed columns:
+// their bound), the row multiplier yu, and where this lane's unknowns sit in
+// the eliminated system (for reading the parametric columns).
+struct AsSol {
+  double xu, yu;
+  int N, W1, pF, pR, myrow;
+  bool fr, ac;
+};
+
+// step 2: the KKT system of the active set in LDS (kkt: N(N+1+Ka) doubles
+// with N <= n+m, cpos: n ints, xs: n doubles of scratch), reduced to
+// Gauss-Jordan form.  Column N is the right-hand side of the current
+// objective; columns N+1+k (k < Ka) are the parametric right-hand sides
+// d rhs / d h_k for the PH term h_k = w_on W_k - prox_on rho_k xbar_k of
+// nonant slot k (-DC at the stationarity row of the slot's column when it
+// is free), so that after the solve u(h) = u + sum_k (h_k - h_cur_k) D_k
+// with D_k = as_col(N+1+k) for as long as the active set holds.  kslot is
+// the nonant slot of column `lane` (-1: none).  kkt stays valid until the
+// next call.
+__device__ AsSol active_set_solve(int lane, int n, int m, const ActiveSet &as, double G, double Q,
+                                  double L, double U, double RL, double RU, double DCl, int kslot,
+                                  int Ka, const int32_t *__restrict__ row_ptr,
+                                  const int32_t *__restrict__ col_idx, const double *vs,
+                                  double *kkt, int *cpos, double *xs) {
+  AsSol r;
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  r.fr = lane < n && as.cs == 0;
+  r.ac = lane < m && as.rs != 0;
+  const unsigned long long fm = __ballot(r.fr), am = __ballot(r.ac);
+  const int nF = __popcll(fm), nR = __popcll(am);
+  const int N = nF + nR, W1 = N + 1 + Ka;
+  r.N = N;
+  r.W1 = W1;
+  r.pF = __popcll(fm & below);
+  r.pR = nF + __popcll(am & below);
+  if (lane < n) {
+    cpos[lane] = r.fr ? r.pF : -1;
+    xs[lane] = as.cs == 1 ? L : (as.cs == 2 ? U : 0.0);
+  }
+  for (int q = lane; q < N * W1; q += WAVE) kkt[q] = 0.0;
+  __syncthreads();
+  if (r.fr) {
+    kkt[r.pF * W1 + r.pF] = Q;
+    kkt[r.pF * W1 + N] = -G;
+    if (kslot >= 0 && kslot < Ka) kkt[r.pF * W1 + N + 1 + kslot] = -DCl;
+  }
+  if (r.ac) {
+    double rhs = as.rs == 1 ? RL : RU;
+    for (int p = row_ptr[lane]; p < row_ptr[lane + 1]; ++p) {
+      const int j = col_idx[p];
+      const double av = vs[p];
+      const int e = cpos[j];
+      if (e >= 0) {
+        kkt[r.pR * W1 + e] = av;
+        kkt[e * W1 + r.pR] = -av;
+      } else {
+        rhs -= av * xs[j];
+      }
+    }
+    kkt[r.pR * W1 + N] = rhs;
+  }
+  __syncthreads();
+  double amax = 0.0;
+  for (int q = lane; q < N * W1; q += WAVE)
+    if (q % W1 < N) amax = fmax(amax, fabs(kkt[q]));
+  amax = wave_max(amax);
+  const double piv_min = 1e-11 * (amax > 0.0 ? amax : 1.0);
+  // lane owns matrix columns lane and lane + WAVE (W1 <= 2 * WAVE)
+  const bool c0 = lane < W1, c1 = lane + WAVE < W1;
+  int pr = 0;
+  r.myrow = -1;
+  for (int kk = 0; kk < N && pr < N; ++kk) {
+    double pv = (lane >= pr && lane < N) ? fabs(kkt[lane * W1 + kk]) : -1.0;
+    int pi = lane;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(pv, off, WAVE);
+      const int oi = __shfl_xor(pi, off, WAVE);
+      if (ov > pv || (ov == pv && oi < pi)) {
+        pv = ov;
+        pi = oi;
+      }
+    }
+    if (!(pv > piv_min)) continue;  // dependent column: its unknown stays 0
+    if (pi != pr) {
+      if (c0) {
+        const double t0 = kkt[pr * W1 + lane];
+        kkt[pr * W1 + lane] = kkt[pi * W1 + lane];
+        kkt[pi * W1 + lane] = t0;
+      }
+      if (c1) {
+        const double t1 = kkt[pr * W1 + lane + WAVE];
+        kkt[pr * W1 + lane + WAVE] = kkt[pi * W1 + lane + WAVE];
+        kkt[pi * W1 + lane + WAVE] = t1;
+      }
+    }
+    __syncthreads();
+    const double piv = kkt[pr * W1 + kk];
+    const double rk0 = c0 ? kkt[pr * W1 + lane] / piv : 0.0;
+    const double rk1 = c1 ? kkt[pr * W1 + lane + WAVE] / piv : 0.0;
+    __syncthreads();
+    if (c0) kkt[pr * W1 + lane] = rk0;
+    if (c1) kkt[pr * W1 + lane + WAVE] = rk1;
+    for (int rr = 0; rr < N; ++rr) {
+      if (rr == pr) continue;
+      const double f = kkt[rr * W1 + kk];
+      if (f != 0.0) {
+        if (c0) kkt[rr * W1 + lane] -= f * rk0;
+        if (c1) kkt[rr * W1 + lane + WAVE] -= f * rk1;
+      }
+    }
+    if (lane == kk) r.myrow = pr;
+    ++pr;
+    __syncthreads();
+  }
+  const double usol = (lane < N && r.myrow >= 0) ? kkt[r.myrow * W1 + N] : 0.0;
+  const double uf = __shfl(usol, r.fr ? r.pF : 0, WAVE);
+  const double ur = __shfl(usol, r.ac ? r.pR : 0, WAVE);
+  r.xu = 0.0;
+  r.yu = 0.0;
+  if (lane < n) r.xu = r.fr ? uf : xs[lane];
+  if (lane < m) r.yu = r.ac ? ur : 0.0;
+  __syncthreads();
+  return r;
+}
+
+// Column q of the solved system, as (column value dx, row value dy) of this
+// lane's column and row (0 for fixed columns and inactive rows).
+__device__ __forceinline__ void as_col(int lane, const AsSol &r, const double *kkt, int q,
+                                       double &dx, double &dy) {
+  const double usol = (lane < r.N && r.myrow >= 0) ? kkt[r.myrow * r.W1 + q] : 0.0;
+  const double uf = __shfl(usol, r.fr ? r.pF : 0, WAVE);
+  const double ur = __shfl(usol, r.ac ? r.pR : 0, WAVE);
+  dx = r.fr ? uf : 0.0;
+  dy = r.ac ? ur : 0.0;
+}
+
+// ------------------------------------------------------------------------
+// Active-set cache.  PH changes only the linear term between solves (W and
+// xbar enter g; Q = prox_on*rho, the bounds and the matrix stay), so while a
+// scenario's optimal active set holds, its solution is an affine function of
+// the K PH terms h_k.  After every successful polish the scenario's
+//   keys[K]      scaled Q of each nonant column (the system the map belongs to)
+//   base[n+m]    u(h = 0): column values, then row multipliers
+//   D[K][n+m]    d u / d h_k
+// are stored (scaled space, scenario-slowest, CW = K + (K+1)(n+m) doubles per
+// scenario), and the next solve first tries u(h) = base + sum_k h_k D_k
+// with the full KKT check (active_set_kernel): one streaming pass over
+// the cache instead of a factorisation.
+// ------------------------------------------------------------------------
+// (SolveArgs::K, CW, nonant_col [K], cache [S][CW], cache_ok [S])
+
+// Store the affine map of the active set just solved (r, kkt) at the
+// current h (HL = this lane's h when its column is a nonant, Ql its scaled Q).
+__device__ void cache_store(int lane, int n, int m, const SolveArgs &c, int s, const AsSol &r,
+                            const double *kkt, double XU, double YU, double HL, double Ql) {
+  double *cs = c.cache + (size_t)s * c.CW;
+  const int K = c.K, NM = n + m;
+  double bx = XU, by = YU;
+  for (int k = 0; k < K; ++k) {
+    const int jk = c.nonant_col[k];
+    const double hk = __shfl(HL, jk, WAVE);
+    double dx, dy;
+    as_col(lane, r, kkt, r.N + 1 + k, dx, dy);
+    bx -= hk * dx;
+    by -= hk * dy;
+    double *Dk = cs + K + (size_t)(k + 1) * NM;
+    if (lane < n) Dk[lane] = dx;
+    if (lane < m) Dk[n + lane] = dy;
+  }
+  const int jl = lane < K ? c.nonant_col[lane] : 0;
+  const double key = __shfl(Ql, jl, WAVE);
+  if (lane < K) cs[lane] = key;
+  if (lane < n) cs[K + lane] = bx;
+  if (lane < m) cs[K + n + lane] = by;
+  if (lane == 0) c.cache_ok[s] = 1;
+}
+
+// ------------------------------------------------------------------------
 // PDHG solve kernel: one workgroup per scenario, everything on chip.
 // P = columns and rows owned per thread, E = extra chunk slots per thread.
 // ------------------------------------------------------------------------
@@ -348,6 +654,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   constexpr bool POL = (BLOCK == WAVE && P == 1);  // polish needs lane == line
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int s = blockIdx.x;
+  if (a.done && a.done[s]) return;  // finished by polish_kernel (whole block exits)
   const int T = blockDim.x;
   const int tid = threadIdx.x;
   const int S = a.S, n = a.n, m = a.m;
@@ -374,6 +681,8 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   // ---- column state in registers
   double X[CPT], Z0X[CPT], G[CPT], Q[CPT], L[CPT], U[CPT], DC[CPT], XN[CPT];
   double cst = 0.0, gsq = 0.0;
+  double HL = 0.0;  // PH term h of column `tid` (polish / cache only)
+  int kslot = -1;
 #pragma unroll
   for (int b = 0; b < CPT; ++b) {
     int j = tid + b * T;
@@ -387,9 +696,14 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
       if (k >= 0) {
         double W = a.W[(size_t)k * S + s], r = a.rho[(size_t)k * S + s];
         double xb = a.xbar[(size_t)k * S + s];
-        g += a.w_on * W - a.prox_on * r * xb;
+        const double h = a.w_on * W - a.prox_on * r * xb;
+        g += h;
         q = a.prox_on * r;
         cst += a.prox_on * 0.5 * r * xb * xb;
+        if (b == 0) {
+          HL = h;
+          kslot = k;
+        }
       }
       DC[b] = dcj;
       G[b] = g * dcj;
@@ -491,70 +805,29 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   // YN.  v[0..5] = primal residual^2, dual residual^2, primal objective,
   // dual objective, |b|^2, |g|^2.  Contains the column products' barrier.
   auto kkt_local = [&](double (&v)[10]) {
-    double pr2 = 0.0, dr2 = 0.0, po = 0.0, dob = 0.0, bl2 = 0.0, g2 = 0.0;
+    for (int i = 0; i < 6; ++i) v[i] = 0.0;
     CL.dots(ys, part_c, DOT);
 #pragma unroll
     for (int b = 0; b < CPT; ++b) {
       int j = tid + b * T;
       LAM[b] = 0.0;
-      if (j < n) {
-        LAM[b] = Q[b] * XN[b] + G[b] - DOT[b];
-        double lam = LAM[b] / DC[b];  // unscaled reduced cost
-        double xu = XN[b] * DC[b];
-        double lu = L[b] * DC[b], uu = U[b] * DC[b];
-        double lp = isfinite(lu) ? fmax(lam, 0.0) : 0.0;
-        double lm = isfinite(uu) ? fmin(lam, 0.0) : 0.0;
-        double rd = lam - lp - lm;
-        dr2 += rd * rd;
-        double qx = Q[b] / (DC[b] * DC[b]);
-        double gu = G[b] / DC[b];
-        po += 0.5 * qx * xu * xu + gu * xu;
-        dob += -0.5 * qx * xu * xu + (lp > 0.0 ? lp * lu : 0.0) + (lm < 0.0 ? lm * uu : 0.0);
-        g2 += gu * gu;
-      }
+      if (j < n) kkt_terms_col(XN[b], G[b], Q[b], L[b], U[b], DC[b], DOT[b], LAM[b], v);
     }
 #pragma unroll
     for (int b = 0; b < RPT; ++b) {
       int i = tid + b * T;
-      if (i < m) {
-        double axu = AXN[b] / DR[b];
-        double rlu = RL[b] / DR[b], ruu = RU[b] / DR[b];
-        double rp = axu - clampd(axu, rlu, ruu);
-        pr2 += rp * rp;
-        double yu = YN[b] * DR[b];
-        dob += (yu > 0.0 ? yu * rlu : 0.0) + (yu < 0.0 ? yu * ruu : 0.0);
-        if (isfinite(rlu)) bl2 += rlu * rlu;
-      }
+      if (i < m) kkt_terms_row(AXN[b], YN[b], RL[b], RU[b], DR[b], v);
     }
-    v[0] = pr2; v[1] = dr2; v[2] = po; v[3] = dob; v[4] = bl2; v[5] = g2;
   };
   // relative primal residual, dual residual and gap from block-summed terms;
   // records the objectives and the diagnostics
   auto kkt_measures = [&](const double (&v)[10], double &ep, double &ed, double &eg) {
-    ep = sqrt(v[0]) / (1.0 + sqrt(v[4]));
-    ed = sqrt(v[1]) / (1.0 + sqrt(v[5]));
-    const double P0 = v[2] + cst, D0 = v[3] + cst;
-    eg = fabs(P0 - D0) / (1.0 + fabs(P0) + fabs(D0));
-    out_pobj = P0;
-    out_dobj = D0;
+    kkt_rel(v, cst, ep, ed, eg, out_pobj, out_dobj);
     d_ep = ep; d_ed = ed; d_eg = eg;
   };
 
-  // Active-set polish (one-wave scenarios, n + m <= POLISH_MAX; lane t owns
-  // column t and row t).  A primal-dual active-set iteration on the exact
-  // KKT system:
-  //  1. classify the trial point: column at a bound when it lies within th
-  //     (relative) of it, row active when its multiplier is nonzero beyond
-  //     th relative to the largest one (|y| > th*max|y|);
-  //  2. solve  q_F x_F - A_RF' y_R = -g_F,  A_RF x_F = b_R - A_R,fixed x_fixed
-  //     by Gauss-Jordan elimination with partial pivoting in LDS (lane =
-  //     matrix column); dependent columns (degenerate duplicate constraints,
-  //     e.g. a row that repeats a variable bound) get the value 0;
-  //  3. accept the clipped point when the full KKT check passes at a.tol,
-  //     else re-classify by the primal-dual active-set rule
-  //       at lower  <=>  lambda + (l - x) > 0,   row at rl <=> y + (rl - Ax) > 0
-  //     and repeat (at most `rounds` solves, stopping on a repeated set).
-  // On success XN/YN/AXN hold the exact point; on failure they are restored.
+  // Active-set polish of a PDHG trial point (see active_set_solve).  On
+  // success XN/YN/AXN hold the exact point; on failure they are restored.
   unsigned long long pol_first[4] = {~0ull, ~0ull, ~0ull, ~0ull};
   auto polish_run = [&](double th, int rounds) -> bool {
     if constexpr (!POL) {
@@ -563,118 +836,22 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
       const int lane = tid;
       const double sx = XN[0], sy = YN[0], sa = AXN[0], sl = LAM[0];
       double *kkt = red + MAX_WAVES * 10;
-      int *cpos = (int *)(kkt + (size_t)(n + m) * (n + m + 1));
-      // ---- 1. initial classification
-      double sc_y = (lane < m) ? fabs(YN[0]) : 0.0;
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) sc_y = fmax(sc_y, __shfl_xor(sc_y, off, WAVE));
-      int cs = 0;  // 0 free, 1 at L, 2 at U
-      if (lane < n) {
-        const double xv = XN[0];
-        if (L[0] == U[0]) cs = 1;
-        else if (isfinite(L[0]) && xv - L[0] <= th * (1.0 + fabs(L[0]))) cs = 1;
-        else if (isfinite(U[0]) && U[0] - xv <= th * (1.0 + fabs(U[0]))) cs = 2;
-      }
-      int rs = 0;  // 0 inactive, 1 at rl, 2 at ru
-      if (lane < m) {
-        if (RL[0] == RU[0]) rs = 1;
-        else if (isfinite(RL[0]) && YN[0] > th * sc_y) rs = 1;
-        else if (isfinite(RU[0]) && YN[0] < -th * sc_y) rs = 2;
-      }
-      {
-        const unsigned long long m0 = __ballot(cs == 1), m1 = __ballot(cs == 2);
-        const unsigned long long m2 = __ballot(rs == 1), m3 = __ballot(rs == 2);
-        if (m0 == pol_first[0] && m1 == pol_first[1] && m2 == pol_first[2] && m3 == pol_first[3])
-          return false;  // this starting set was tried already
-        pol_first[0] = m0; pol_first[1] = m1; pol_first[2] = m2; pol_first[3] = m3;
-      }
-      unsigned long long prev[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-      const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      int *cpos = (int *)(kkt + (size_t)(n + m) * (n + m + 1 + (a.cache ? a.K : 0)));
+      ActiveSet as = classify_trial(lane, n, m, th, XN[0], YN[0], L[0], U[0], RL[0], RU[0]);
+      unsigned long long sig[4], prev[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+      as.signature(sig);
+      if (same_sig(sig, pol_first)) return false;  // this starting set was tried already
+      for (int i = 0; i < 4; ++i) pol_first[i] = sig[i];
       for (int round = 0; round < rounds; ++round) {
-        const unsigned long long m0 = __ballot(cs == 1), m1 = __ballot(cs == 2);
-        const unsigned long long m2 = __ballot(rs == 1), m3 = __ballot(rs == 2);
-        if (m0 == prev[0] && m1 == prev[1] && m2 == prev[2] && m3 == prev[3]) break;  // cycle
-        prev[0] = m0; prev[1] = m1; prev[2] = m2; prev[3] = m3;
-        // ---- 2. KKT system of the active set
-        const bool fr = lane < n && cs == 0;
-        const bool ac = lane < m && rs != 0;
-        const unsigned long long fm = __ballot(fr), am = __ballot(ac);
-        const int nF = __popcll(fm), nR = __popcll(am);
-        const int N = nF + nR, W1 = N + 1;
-        const int pF = __popcll(fm & below), pR = nF + __popcll(am & below);
-        if (lane < n) {
-          cpos[lane] = fr ? pF : -1;
-          xs[lane] = cs == 1 ? L[0] : (cs == 2 ? U[0] : 0.0);
-        }
-        for (int q = lane; q < N * W1; q += WAVE) kkt[q] = 0.0;
-        __syncthreads();
-        if (fr) {
-          kkt[pF * W1 + pF] = Q[0];
-          kkt[pF * W1 + N] = -G[0];
-        }
-        if (ac) {
-          double rhs = rs == 1 ? RL[0] : RU[0];
-          for (int p = a.P.row_ptr[lane]; p < a.P.row_ptr[lane + 1]; ++p) {
-            const int j = a.P.col_idx[p];
-            const double av = vs[p];
-            const int e = cpos[j];
-            if (e >= 0) {
-              kkt[pR * W1 + e] = av;
-              kkt[e * W1 + pR] = -av;
-            } else {
-              rhs -= av * xs[j];
-            }
-          }
-          kkt[pR * W1 + N] = rhs;
-        }
-        __syncthreads();
-        double amax = 0.0;
-        for (int q = lane; q < N * W1; q += WAVE) amax = fmax(amax, fabs(kkt[q]));
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) amax = fmax(amax, __shfl_xor(amax, off, WAVE));
-        const double piv_min = 1e-11 * (amax > 0.0 ? amax : 1.0);
-        int pr = 0, myrow = -1;
-        for (int kk = 0; kk < N && pr < N; ++kk) {
-          double pv = (lane >= pr && lane < N) ? fabs(kkt[lane * W1 + kk]) : -1.0;
-          int pi = lane;
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) {
-            const double ov = __shfl_xor(pv, off, WAVE);
-            const int oi = __shfl_xor(pi, off, WAVE);
-            if (ov > pv || (ov == pv && oi < pi)) {
-              pv = ov;
-              pi = oi;
-            }
-          }
-          if (!(pv > piv_min)) continue;  // dependent column: its unknown stays 0
-          if (pi != pr && lane <= N) {
-            const double t0 = kkt[pr * W1 + lane];
-            kkt[pr * W1 + lane] = kkt[pi * W1 + lane];
-            kkt[pi * W1 + lane] = t0;
-          }
-          __syncthreads();
-          const double piv = kkt[pr * W1 + kk];
-          const double rk = lane <= N ? kkt[pr * W1 + lane] / piv : 0.0;
-          __syncthreads();
-          if (lane <= N) kkt[pr * W1 + lane] = rk;
-          for (int rr = 0; rr < N; ++rr) {
-            if (rr == pr) continue;
-            const double f = kkt[rr * W1 + kk];
-            if (f != 0.0 && lane <= N) kkt[rr * W1 + lane] -= f * rk;
-          }
-          if (lane == kk) myrow = pr;
-          ++pr;
-          __syncthreads();
-        }
-        const double usol = (lane < N && myrow >= 0) ? kkt[myrow * W1 + N] : 0.0;
-        const double uf = __shfl(usol, fr ? pF : 0, WAVE);
-        const double ur = __shfl(usol, ac ? pR : 0, WAVE);
-        double XU = 0.0;
-        if (lane < n) XU = fr ? uf : xs[lane];
-        if (lane < m) YN[0] = ac ? ur : 0.0;
-        // ---- 3. check the clipped point
+        as.signature(sig);
+        if (same_sig(sig, prev)) break;  // cycle
+        for (int i = 0; i < 4; ++i) prev[i] = sig[i];
+        const AsSol r = active_set_solve(lane, n, m, as, G[0], Q[0], L[0], U[0], RL[0], RU[0],
+                                         DC[0], kslot, a.cache ? a.K : 0, a.P.row_ptr,
+                                         a.P.col_idx, vs, kkt, cpos, xs);
+        const double XU = r.xu, YU = r.yu;
+        if (lane < m) YN[0] = YU;
         if (lane < n) XN[0] = clampd(XU, L[0], U[0]);
-        __syncthreads();
         if (lane < n) xs[lane] = XN[0];
         if (lane < m) ys[lane] = YN[0];
         __syncthreads();
@@ -686,8 +863,10 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
         block_sum<10>(v, red);
         double ep, ed, eg;
         kkt_measures(v, ep, ed, eg);
-        if (ep <= a.tol && ed <= a.tol && eg <= a.tol) return true;
-        // ---- primal-dual active-set update from the unclipped solution
+        if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
+          if (a.cache) cache_store(lane, n, m, a, s, r, kkt, XU, YU, HL, Q[0]);
+          return true;
+        }
         const bool clipped = __ballot(lane < n && XU != XN[0]) != 0ull;
         double AXU = AXN[0];
         const double LAMU = LAM[0] + Q[0] * (XU - XN[0]);
@@ -699,18 +878,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
           AXU = DOT[0];
         }
         __syncthreads();
-        if (lane < n) {
-          if (L[0] == U[0]) cs = 1;
-          else if (isfinite(L[0]) && LAMU + (L[0] - XU) > 0.0) cs = 1;
-          else if (isfinite(U[0]) && -LAMU + (XU - U[0]) > 0.0) cs = 2;
-          else cs = 0;
-        }
-        if (lane < m) {
-          if (RL[0] == RU[0]) rs = 1;
-          else if (isfinite(RL[0]) && YN[0] + (RL[0] - AXU) > 0.0) rs = 1;
-          else if (isfinite(RU[0]) && -YN[0] + (AXU - RU[0]) > 0.0) rs = 2;
-          else rs = 0;
-        }
+        as = classify_pdas(lane, n, m, XU, LAMU, YN[0], AXU, L[0], U[0], RL[0], RU[0]);
       }
       XN[0] = sx;
       YN[0] = sy;
@@ -722,6 +890,8 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   };
 
   // warm start: the previous PH iteration's active set usually still holds
+  // (when the affine map of active_set_kernel did not, the set changed only
+  // a little: a few primal-dual active-set rounds from the warm point)
   if constexpr (POL) {
     if (a.polish && a.warm) {
 #pragma unroll
@@ -731,8 +901,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
         YN[b] = Y[b];
         AXN[b] = AX[b];
       }
-      bool ok = polish_run(1e-9, POLISH_ROUNDS);
-      if (ok) {
+      if (polish_run(1e-9, POLISH_ROUNDS)) {
         stat = PH_STATUS_OPTIMAL;
         how = 1;
 #pragma unroll
@@ -741,8 +910,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
         for (int b = 0; b < RPT; ++b) Y[b] = YN[b];
         maxit_eff = 0;
       } else {
-        // restore ys <- Y for the iteration
-        if (tid < m) ys[tid] = Y[0];
+        if (tid < m) ys[tid] = Y[0];  // restore ys <- Y for the iteration
         __syncthreads();
       }
     }
@@ -924,17 +1092,128 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     a.diag[PH_DIAG_W * s + 2] = d_eg;
     a.diag[PH_DIAG_W * s + 3] = d_r;
     a.diag[PH_DIAG_W * s + 4] = (double)how;
-    if (stat != PH_STATUS_OPTIMAL) atomicAdd(&a.summary[0], 1ull);
-    atomicAdd(&a.summary[1], (unsigned long long)it);
-    atomicMax(&a.summary[2], (unsigned long long)it);
-    if (how) atomicAdd(&a.summary[3], 1ull);
+  }
+}
+
+// ------------------------------------------------------------------------
+// Active-set cache kernel: one wave per scenario, WPB scenarios per block.
+// Applies the cached affine map u(h) = base + sum_k h_k D_k of the
+// scenario's last optimal active set to the current PH terms, clips, and
+// runs the full KKT check at a.tol (the same acceptance test as PDHG).
+// Accepted scenarios are written out and marked done; the rest (no valid
+// entry, Q changed, or the active set moved) go to pdhg_kernel, whose warm
+// polish refreshes the entry.  Streams CW doubles of cache per scenario.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int WPB>
+__global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a, int32_t *done) {
+  __shared__ double sh[WPB][2 * WAVE];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w = threadIdx.x / WAVE;
+  const int s = blockIdx.x * WPB + w;
+  if (s >= a.S) return;  // wave-uniform; the kernel has no block barriers
+  const int S = a.S, n = a.n, m = a.m, K = a.K, NM = n + m;
+  double *xs = sh[w];
+  double *ys = sh[w] + WAVE;
+  if (!a.cache_ok[s]) {
+    if (lane == 0) done[s] = 0;
+    return;
+  }
+  const double *cs = a.cache + (size_t)s * a.CW;
+  // column state (scaled, as pdhg_kernel)
+  double G = 0.0, Q = 0.0, L = 0.0, U = 0.0, DC = 1.0, HL = 0.0, cstl = 0.0;
+  bool keybad = false;
+  if (lane < n) {
+    const int j = lane;
+    DC = a.dc[(size_t)s * n + j];
+    double g = a.c[(size_t)j * S + s], q = 0.0;
+    const int k = a.slot_of_col[j];
+    if (k >= 0) {
+      const double W = a.W[(size_t)k * S + s], r = a.rho[(size_t)k * S + s];
+      const double xb = a.xbar[(size_t)k * S + s];
+      HL = a.w_on * W - a.prox_on * r * xb;
+      g += HL;
+      q = a.prox_on * r;
+      cstl = a.prox_on * 0.5 * r * xb * xb;
+    }
+    G = g * DC;
+    Q = q * DC * DC;
+    L = a.l[(size_t)j * S + s] / DC;
+    U = a.u[(size_t)j * S + s] / DC;
+    if (k >= 0) keybad = cs[k] != Q;
+  }
+  if (__ballot(keybad)) {  // the entry belongs to another prox term
+    if (lane == 0) done[s] = 0;
+    return;
+  }
+  double RL = 0.0, RU = 0.0, DR = 1.0;
+  if (lane < m) {
+    DR = a.dr[(size_t)s * m + lane];
+    RL = a.rl[(size_t)lane * S + s] * DR;
+    RU = a.ru[(size_t)lane * S + s] * DR;
+  }
+  // u(h)
+  double XU = lane < n ? cs[K + lane] : 0.0;
+  double YU = lane < m ? cs[K + n + lane] : 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double hk = __shfl(HL, a.nonant_col[k], WAVE);
+    const double *Dk = cs + K + (size_t)(k + 1) * NM;
+    if (lane < n) XU = fma(hk, Dk[lane], XU);
+    if (lane < m) YU = fma(hk, Dk[n + lane], YU);
+  }
+  const double XN = lane < n ? clampd(XU, L, U) : 0.0;
+  const double YN = YU;
+  if (lane < n) xs[lane] = XN;
+  if (lane < m) ys[lane] = YN;
+  wsync();
+  const double *vs = a.vals_s + (size_t)s * a.nnz;
+  double AXN = 0.0, ATY = 0.0;
+  if (lane < m)
+    for (int p = a.P.row_ptr[lane]; p < a.P.row_ptr[lane + 1]; ++p)
+      AXN = fma(vs[p], xs[a.P.col_idx[p]], AXN);
+  if (lane < n)
+    for (int p = a.P.col_ptr[lane]; p < a.P.col_ptr[lane + 1]; ++p)
+      ATY = fma(vs[a.P.csc_k[p]], ys[a.P.csc_row[p]], ATY);
+  double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double lam;
+  if (lane < n) kkt_terms_col(XN, G, Q, L, U, DC, ATY, lam, v);
+  if (lane < m) kkt_terms_row(AXN, YN, RL, RU, DR, v);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[i] = wave_sum(v[i]);
+  const double cst = wave_sum(cstl);
+  double ep, ed, eg, pobj, dobj;
+  kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
+  const bool ok = ep <= a.tol && ed <= a.tol && eg <= a.tol;
+  if (!ok) {
+    if (lane == 0) done[s] = 0;
+    return;
+  }
+  if (lane < n) a.x[(size_t)lane * S + s] = XN * DC;
+  if (lane < m) a.y[(size_t)lane * S + s] = YN * DR;
+  if (lane == 0) {
+    done[s] = 1;
+    a.status[s] = PH_STATUS_OPTIMAL;
+    a.iters[s] = 0;
+    a.pobj[s] = pobj;
+    a.dbound[s] = dobj;
+    double *dg = a.diag + PH_DIAG_W * (size_t)s;
+    dg[0] = ep;
+    dg[1] = ed;
+    dg[2] = eg;
+    dg[3] = -1.0;
+    dg[4] = 3.0;
   }
 }
 
 // ------------------------------------------------------------------------
 // nonanticipativity kernels (scenario-fastest, coalesced)
 // ------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) xbar_accum_kernel(
+__global__ void __launch_bounds__(1024) xbar_accum_kernel(
     int S, const double *__restrict__ x, const double *__restrict__ pc,
     const int32_t *__restrict__ nonant_col, const int32_t *__restrict__ slot_k,
     const int32_t *__restrict__ s0, const int32_t *__restrict__ s1, int G,
@@ -984,7 +1263,7 @@ __global__ void __launch_bounds__(256) update_w_kernel(
   absdiff[s] = acc;
 }
 
-__global__ void __launch_bounds__(256) segment_sum_kernel(
+__global__ void __launch_bounds__(1024) segment_sum_kernel(
     const double *__restrict__ v, const double *__restrict__ w,
     const int32_t *__restrict__ seg, double *__restrict__ out) {
   __shared__ double red[MAX_WAVES];
@@ -994,6 +1273,44 @@ __global__ void __launch_bounds__(256) segment_sum_kernel(
     acc[0] += w ? w[s] * v[s] : v[s];
   block_sum<1>(acc, red);
   if (threadIdx.x == 0) out[r] = acc[0];
+}
+
+// One block: (not optimal, sum iters, max iters, polished) of the last solve.
+// A reduction instead of per-workgroup atomics on one address, which
+// serialise 10k+ workgroups at the end of the solve.
+__global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__restrict__ status,
+                                                       const int32_t *__restrict__ iters,
+                                                       const double *__restrict__ diag,
+                                                       unsigned long long *__restrict__ out) {
+  __shared__ unsigned long long red[4][MAX_WAVES];
+  unsigned long long v[4] = {0ull, 0ull, 0ull, 0ull};
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    const unsigned long long it = (unsigned long long)iters[s];
+    v[0] += status[s] != PH_STATUS_OPTIMAL;
+    v[1] += it;
+    v[2] = it > v[2] ? it : v[2];
+    v[3] += diag[PH_DIAG_W * (size_t)s + 4] != 0.0;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned long long o = __shfl_xor(v[i], off, WAVE);
+      v[i] = i == 2 ? (o > v[i] ? o : v[i]) : v[i] + o;
+    }
+  }
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  if (lane == 0)
+    for (int i = 0; i < 4; ++i) red[i][wid] = v[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x / WAVE;
+    for (int i = 0; i < 4; ++i) {
+      unsigned long long t = red[i][0];
+      for (int w = 1; w < nw; ++w) t = i == 2 ? (red[i][w] > t ? red[i][w] : t) : t + red[i][w];
+      out[i] = t;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(256) eval_obj_kernel(
@@ -1032,6 +1349,10 @@ struct ph_batch {
   double *d_c = nullptr, *d_l = nullptr, *d_u = nullptr, *d_rl = nullptr, *d_ru = nullptr;
   double *d_diag = nullptr;
   unsigned long long *d_summary = nullptr;
+  // active-set cache (polish-size scenarios): [S][CW] doubles + flags
+  int CW = 0;
+  double *d_cache = nullptr;
+  int32_t *d_cache_ok = nullptr, *d_done = nullptr;
   // extra chunks of lines longer than LINE_D (see LineRegs)
   int xr = 0, xc = 0;
   int32_t *d_r_pb = nullptr, *d_r_pos = nullptr, *d_r_len = nullptr;
@@ -1206,9 +1527,10 @@ static bool polish_fits(const ph_batch *b) {
 static size_t solve_lds_bytes(const ph_batch *b) {
   size_t d = (size_t)b->n + b->m + b->xr + b->xc + MAX_WAVES * 10;
   size_t extra = 0;
-  if (polish_fits(b)) {  // KKT matrix + free-column positions
+  if (polish_fits(b)) {  // KKT matrix (+ parametric columns) + free-column positions
     const size_t N = (size_t)b->n + b->m;
-    extra = sizeof(double) * N * (N + 1) + sizeof(int32_t) * b->n;
+    const size_t Ka = b->d_cache ? (size_t)b->K : 0;
+    extra = sizeof(double) * N * (N + 1 + Ka) + sizeof(int32_t) * b->n;
   }
   return sizeof(double) * d + extra;
 }
@@ -1227,6 +1549,7 @@ int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const doubl
   }
   const size_t lds = scale_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_batch_bind: scenario does not fit in LDS (nnz+2n+2m too large)");
+  if (b->d_cache_ok) HIP_OK(hipMemsetAsync(b->d_cache_ok, 0, sizeof(int32_t) * b->S, b->stream));
   Pattern P{b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k};
   DISPATCH_GEOM(b->block, b->per, 0, {
     hipLaunchKernelGGL((scale_kernel<B_, P_, P_>), dim3(b->S), dim3(B_), lds, b->stream,
@@ -1251,8 +1574,21 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
   if (rc) return rc;
   HIP_OK(hipMemcpyAsync(b->d_nonant_col, nonant_col, sizeof(int32_t) * (K ? K : 0), hipMemcpyHostToDevice, b->stream));
   HIP_OK(hipMemcpyAsync(b->d_slot_of_col, slot.data(), sizeof(int32_t) * b->n, hipMemcpyHostToDevice, b->stream));
-  HIP_OK(hipStreamSynchronize(b->stream));
   b->K = K;
+  // active-set cache for scenarios the one-wave polish covers
+  for (void *p : {(void *)b->d_cache, (void *)b->d_cache_ok, (void *)b->d_done})
+    if (p) (void)hipFree(p);
+  b->d_cache = nullptr;
+  b->d_cache_ok = b->d_done = nullptr;
+  b->CW = 0;
+  if (polish_fits(b)) {
+    b->CW = K + (K + 1) * (b->n + b->m);
+    if ((rc = dalloc(&b->d_cache, (size_t)b->S * b->CW)) || (rc = dalloc(&b->d_cache_ok, b->S)) ||
+        (rc = dalloc(&b->d_done, b->S)))
+      return rc;
+    HIP_OK(hipMemsetAsync(b->d_cache_ok, 0, sizeof(int32_t) * b->S, b->stream));
+  }
+  HIP_OK(hipStreamSynchronize(b->stream));
   return PH_OK;
 }
 
@@ -1273,20 +1609,35 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.slot_of_col = b->d_slot_of_col;
   a.W = W; a.rho = rho; a.xbar = xbar; a.w_on = w_on; a.prox_on = prox_on;
   a.x = x; a.y = y; a.omega = omega; a.status = status; a.iters = iters;
-  a.pobj = pobj; a.dbound = dbound; a.diag = b->d_diag; a.summary = b->d_summary;
+  a.pobj = pobj; a.dbound = dbound; a.diag = b->d_diag;
   a.tol = opts ? opts->tol : 1e-9;
   a.max_iters = opts ? opts->max_iters : 200000;
   a.check_every = opts ? opts->check_every : 64;
   a.warm = opts ? opts->warm_start : 1;
   a.refl = opts ? opts->reflection : 1.0;
   a.polish = (opts ? opts->polish : 1) && polish_fits(b);
+  a.K = b->K;
+  a.CW = b->CW;
+  a.nonant_col = b->d_nonant_col;
+  a.cache = a.polish ? b->d_cache : nullptr;
+  a.cache_ok = b->d_cache_ok;
+  a.done = nullptr;
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
-  HIP_OK(hipMemsetAsync(b->d_summary, 0, 4 * sizeof(unsigned long long), b->stream));
+  if (a.cache && a.warm) {
+    constexpr int WPB = 4;
+    hipLaunchKernelGGL((active_set_kernel<WPB>), dim3((b->S + WPB - 1) / WPB), dim3(WPB * WAVE),
+                       0, b->stream, a, b->d_done);
+    HIP_OK(hipGetLastError());
+    a.done = b->d_done;
+  }
   DISPATCH_GEOM(b->block, b->per, b->ext, {
     hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(b->S), dim3(B_), lds, b->stream, a);
   });
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(1024), 0, b->stream, b->S, status, iters,
+                     b->d_diag, b->d_summary);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -1297,7 +1648,7 @@ int ph_xbar_accum(ph_batch_t b, const double *x, const double *prob_coeff, int32
   if (!b || !x || !prob_coeff || G <= 0 || !slot_k || !slot_s0 || !slot_s1 || !out_sums)
     return fail(PH_EINVAL, "ph_xbar_accum: bad arguments");
   if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_xbar_accum: no nonants declared");
-  hipLaunchKernelGGL(xbar_accum_kernel, dim3(G), dim3(256), 0, b->stream, b->S, x, prob_coeff,
+  hipLaunchKernelGGL(xbar_accum_kernel, dim3(G), dim3(1024), 0, b->stream, b->S, x, prob_coeff,
                      b->d_nonant_col, slot_k, slot_s0, slot_s1, G, out_sums);
   HIP_OK(hipGetLastError());
   return PH_OK;
@@ -1318,7 +1669,7 @@ int ph_update_w(ph_batch_t b, const double *x, const double *sums, int32_t G, co
 int ph_segment_sum(ph_batch_t b, const double *v, const double *w, int32_t R, const int32_t *seg,
                    double *out) {
   if (!b || !v || R <= 0 || !seg || !out) return fail(PH_EINVAL, "ph_segment_sum: bad arguments");
-  hipLaunchKernelGGL(segment_sum_kernel, dim3(R), dim3(256), 0, b->stream, v, w, seg, out);
+  hipLaunchKernelGGL(segment_sum_kernel, dim3(R), dim3(1024), 0, b->stream, v, w, seg, out);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -1360,6 +1711,7 @@ void ph_batch_destroy(ph_batch_t b) {
   void *ptrs[] = {b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k,
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
+                  b->d_cache, b->d_cache_ok, b->d_done,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

@@ -29,10 +29,10 @@ def report(tag, ms):
     st = ph.batch.status.cpu().numpy()
     q = np.percentile(it, [50, 90, 99, 99.9])
     how = ph.batch.diagnostics()[:, 4].astype(int)
-    hw = np.bincount(how, minlength=3)
+    hw = np.bincount(how, minlength=4)
     print(f"{tag}: kernel {ms:8.3f} ms  iters mean {it.mean():7.1f} p50 {q[0]:.0f} p90 {q[1]:.0f} "
           f"p99 {q[2]:.0f} p99.9 {q[3]:.0f} max {it.max()}  nonopt {(st != 0).sum()}  "
-          f"sum/max {it.sum()/max(1,it.max()):.0f}  how(tol/warm-polish/polish) {hw.tolist()}", flush=True)
+          f"sum/max {it.sum()/max(1,it.max()):.0f}  how(tol/warm-polish/polish/cache) {hw.tolist()}", flush=True)
 
 
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
