@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -51,8 +52,17 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// A wave-uniform double moved to scalar registers (the compiler cannot
+// tell that values read back from LDS are uniform).
+__device__ __forceinline__ double uniform(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // Block-wide sum of NV values.  `red` is LDS scratch of MAX_WAVES*NV doubles.
-// All threads receive the totals.  Contains two barriers.
+// All threads receive the totals (in scalar registers).  Contains two barriers.
 template <int NV>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double *red) {
   const int lane = threadIdx.x & (WAVE - 1);
@@ -68,7 +78,7 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double *red) {
   for (int i = 0; i < NV; ++i) {
     double t = 0.0;
     for (int w = 0; w < nw; ++w) t += red[w * NV + i];
-    v[i] = t;
+    v[i] = uniform(t);
   }
   __syncthreads();
 }
@@ -219,6 +229,30 @@ __global__ void __launch_bounds__(BLOCK) scale_kernel(
   }
 }
 
+// Per-scenario static block for the one-wave kernels (see SolveArgs::sb).
+__global__ void __launch_bounds__(256) static_block_kernel(
+    int S, int n, int m, const double *__restrict__ c, const double *__restrict__ l,
+    const double *__restrict__ u, const double *__restrict__ rl, const double *__restrict__ ru,
+    const double *__restrict__ dc, const double *__restrict__ dr, double *__restrict__ sb) {
+  const int s = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+  const int lane = threadIdx.x & (WAVE - 1);
+  if (s >= S) return;
+  double *o = sb + (size_t)s * (4 * n + 3 * m);
+  for (int j = lane; j < n; j += WAVE) {
+    const double d = dc[(size_t)s * n + j];
+    o[j] = c[(size_t)j * S + s] * d;
+    o[n + j] = l[(size_t)j * S + s] / d;
+    o[2 * n + j] = u[(size_t)j * S + s] / d;
+    o[3 * n + j] = d;
+  }
+  for (int i = lane; i < m; i += WAVE) {
+    const double d = dr[(size_t)s * m + i];
+    o[4 * n + i] = rl[(size_t)i * S + s] * d;
+    o[4 * n + m + i] = ru[(size_t)i * S + s] * d;
+    o[4 * n + 2 * m + i] = d;
+  }
+}
+
 struct SolveArgs {
   int S, n, m, nnz;
   Pattern P;
@@ -236,12 +270,20 @@ struct SolveArgs {
   int max_iters, check_every, warm;
   double refl;
   int polish;  // 1: one-wave scenario with n + m <= POLISH_MAX and polish enabled
-  // active-set cache (see CacheArgs); cache == null: no caching
+  // per-scenario static block [S][SBW] (scenario-slowest, coalesced for a
+  // wave per scenario): G0 = c*dc [n], l/dc [n], u/dc [n], dc [n],
+  // rl*dr [m], ru*dr [m], dr [m]
+  const double *sb;
+  // active-set cache (see cache_store); cache == null: no caching
   int K, CW;
   const int32_t *nonant_col;
   double *cache;
   int32_t *cache_ok;
-  const int32_t *done;  // [S] or null: 1 = solved by active_set_kernel, skip
+  unsigned long long *hint;  // [S][4] active-set signature for the warm polish
+  int32_t *hint_ok;          // [S] 1 = hint valid
+  // scenarios for pdhg_kernel: wl == null -> all S, else wl[0 .. *wl_count)
+  int32_t *wl, *wl_count;
+  int32_t *queue;  // work-queue counter (0 at launch)
 };
 
 // Active-set polish: largest KKT system (free columns + active rows) and the
@@ -249,6 +291,7 @@ struct SolveArgs {
 constexpr int POLISH_MAX = 63;
 constexpr double POLISH_START = 1e-4;
 constexpr int POLISH_ROUNDS = 6;
+constexpr int GJ_ROWS = 4;  // rows per LDS batch in the Gauss-Jordan elimination
 
 // Matrix entries a thread keeps in VGPRs for the lines (rows or columns) it
 // owns plus the extra chunks of long lines it helps with.  A line's first
@@ -569,12 +612,26 @@ __device__ AsSol active_set_solve(int lane, int n, int m, const ActiveSet &as, d
     __syncthreads();
     if (c0) kkt[pr * W1 + lane] = rk0;
     if (c1) kkt[pr * W1 + lane + WAVE] = rk1;
-    for (int rr = 0; rr < N; ++rr) {
-      if (rr == pr) continue;
-      const double f = kkt[rr * W1 + kk];
-      if (f != 0.0) {
-        if (c0) kkt[rr * W1 + lane] -= f * rk0;
-        if (c1) kkt[rr * W1 + lane + WAVE] -= f * rk1;
+    // eliminate column kk from the other rows, GJ_ROWS rows per batch: all
+    // reads of a batch are issued before its writes (one LDS round trip per
+    // batch instead of one per row)
+    for (int r0 = 0; r0 < N; r0 += GJ_ROWS) {
+      double f[GJ_ROWS], a0[GJ_ROWS], a1[GJ_ROWS];
+#pragma unroll
+      for (int t = 0; t < GJ_ROWS; ++t) {
+        const int rr = r0 + t;
+        const bool on = rr < N && rr != pr;
+        f[t] = on ? kkt[rr * W1 + kk] : 0.0;
+        a0[t] = (on && c0) ? kkt[rr * W1 + lane] : 0.0;
+        a1[t] = (on && c1) ? kkt[rr * W1 + lane + WAVE] : 0.0;
+      }
+#pragma unroll
+      for (int t = 0; t < GJ_ROWS; ++t) {
+        const int rr = r0 + t;
+        if (f[t] != 0.0) {
+          if (c0) kkt[rr * W1 + lane] = a0[t] - f[t] * rk0;
+          if (c1) kkt[rr * W1 + lane + WAVE] = a1[t] - f[t] * rk1;
+        }
       }
     }
     if (lane == kk) r.myrow = pr;
@@ -607,41 +664,188 @@ __device__ __forceinline__ void as_col(int lane, const AsSol &r, const double *k
 // Active-set cache.  PH changes only the linear term between solves (W and
 // xbar enter g; Q = prox_on*rho, the bounds and the matrix stay), so while a
 // scenario's optimal active set holds, its solution is an affine function of
-// the K PH terms h_k.  After every successful polish the scenario's
-//   keys[K]      scaled Q of each nonant column (the system the map belongs to)
-//   base[n+m]    u(h = 0): column values, then row multipliers
-//   D[K][n+m]    d u / d h_k
-// are stored (scaled space, scenario-slowest, CW = K + (K+1)(n+m) doubles per
-// scenario), and the next solve first tries u(h) = base + sum_k h_k D_k
-// with the full KKT check (active_set_kernel): one streaming pass over
-// the cache instead of a factorisation.
+// the K PH terms h_k = w_on W_k - prox_on rho_k xbar_k.  After every
+// successful polish the scenario's map is stored (scaled space,
+// scenario-slowest, CW = K + (K+1)*2(n+m) doubles per scenario):
+//   keys[K]        scaled Q of each nonant column (the system the map is for)
+//   base[2(n+m)]   value at h = 0 of the vector v = (x[n], y[m], A x[m], A'y[n])
+//   D[K][2(n+m)]   d v / d h_k
+// and the next solve first evaluates v(h) = base + sum_k h_k D_k and runs the
+// full KKT check on it (active_set_kernel): one streaming pass over the
+// entry, no factorisation and, while no column needs clipping, no SpMV.
 // ------------------------------------------------------------------------
-// (SolveArgs::K, CW, nonant_col [K], cache [S][CW], cache_ok [S])
+__device__ __forceinline__ int cache_vlen(int n, int m) { return 2 * (n + m); }
+// offsets inside a v vector
+__device__ __forceinline__ int cv_x(int, int) { return 0; }
+__device__ __forceinline__ int cv_y(int n, int) { return n; }
+__device__ __forceinline__ int cv_ax(int n, int m) { return n + m; }
+__device__ __forceinline__ int cv_aty(int n, int m) { return n + 2 * m; }
 
-// Store the affine map of the active set just solved (r, kkt) at the
-// current h (HL = this lane's h when its column is a nonant, Ql its scaled Q).
+// Store the affine map of the active set just solved (r, kkt): XU/YU is the
+// unclipped solution at the current h (HL = this lane's h when its column is
+// a nonant, Ql its scaled Q).  rowdot(xs) / coldot(ys) return row / column
+// `lane` of A xs / A' ys for the vectors the caller put in LDS (single-wave
+// block: __syncthreads is a wave barrier).
+template <class RowDot, class ColDot>
 __device__ void cache_store(int lane, int n, int m, const SolveArgs &c, int s, const AsSol &r,
-                            const double *kkt, double XU, double YU, double HL, double Ql) {
+                            const double *kkt, double XU, double YU, double HL, double Ql,
+                            double *xs, double *ys, RowDot rowdot, ColDot coldot) {
   double *cs = c.cache + (size_t)s * c.CW;
-  const int K = c.K, NM = n + m;
-  double bx = XU, by = YU;
+  const int K = c.K, VL = cache_vlen(n, m);
+  __syncthreads();
+  if (lane < n) xs[lane] = XU;
+  if (lane < m) ys[lane] = YU;
+  __syncthreads();
+  double bx = XU, by = YU, bax = rowdot(), baty = coldot();
   for (int k = 0; k < K; ++k) {
-    const int jk = c.nonant_col[k];
-    const double hk = __shfl(HL, jk, WAVE);
+    const double hk = __shfl(HL, c.nonant_col[k], WAVE);
     double dx, dy;
     as_col(lane, r, kkt, r.N + 1 + k, dx, dy);
+    __syncthreads();
+    if (lane < n) xs[lane] = dx;
+    if (lane < m) ys[lane] = dy;
+    __syncthreads();
+    const double dax = rowdot(), daty = coldot();
+    double *Dk = cs + K + (size_t)(k + 1) * VL;
+    if (lane < n) {
+      Dk[cv_x(n, m) + lane] = dx;
+      Dk[cv_aty(n, m) + lane] = daty;
+    }
+    if (lane < m) {
+      Dk[cv_y(n, m) + lane] = dy;
+      Dk[cv_ax(n, m) + lane] = dax;
+    }
     bx -= hk * dx;
     by -= hk * dy;
-    double *Dk = cs + K + (size_t)(k + 1) * NM;
-    if (lane < n) Dk[lane] = dx;
-    if (lane < m) Dk[n + lane] = dy;
+    bax -= hk * dax;
+    baty -= hk * daty;
   }
   const int jl = lane < K ? c.nonant_col[lane] : 0;
   const double key = __shfl(Ql, jl, WAVE);
+  double *B = cs + K;
   if (lane < K) cs[lane] = key;
-  if (lane < n) cs[K + lane] = bx;
-  if (lane < m) cs[K + n + lane] = by;
+  if (lane < n) {
+    B[cv_x(n, m) + lane] = bx;
+    B[cv_aty(n, m) + lane] = baty;
+  }
+  if (lane < m) {
+    B[cv_y(n, m) + lane] = by;
+    B[cv_ax(n, m) + lane] = bax;
+  }
   if (lane == 0) c.cache_ok[s] = 1;
+  __syncthreads();
+}
+
+// Active set from a stored signature (hint written by active_set_kernel).
+__device__ __forceinline__ ActiveSet set_from_sig(int lane, const unsigned long long *sig) {
+  ActiveSet as{0, 0};
+  const unsigned long long bit = 1ull << lane;
+  as.cs = (sig[0] & bit) ? 1 : ((sig[1] & bit) ? 2 : 0);
+  as.rs = (sig[2] & bit) ? 1 : ((sig[3] & bit) ? 2 : 0);
+  return as;
+}
+
+// ------------------------------------------------------------------------
+// The active-set polish of one scenario on one wave (lane t owns column t
+// and row t, single-wave block), out of line: it runs rarely, and inlined
+// into pdhg_kernel its Gauss-Jordan temporaries would sit on top of the
+// PDHG loop's register state.  Products with A use the shared pattern and
+// the scenario's scaled values in global memory.
+// ------------------------------------------------------------------------
+struct PolishLane {  // scaled data of column `lane` and row `lane`
+  double G, Q, L, U, DC, RL, RU, DR, HL;
+  int kslot;
+};
+struct PolishRes {
+  double XN, YN, AXN, pobj, dobj, ep, ed, eg;
+  unsigned long long first[4];  // the starting set tried (see pol_first)
+  int ok;
+};
+
+__device__ __forceinline__ double pat_rowdot(int lane, int m, const Pattern &P, const double *vs,
+                                             const double *xs) {
+  double acc = 0.0;
+  if (lane < m)
+    for (int p = P.row_ptr[lane]; p < P.row_ptr[lane + 1]; ++p) acc = fma(vs[p], xs[P.col_idx[p]], acc);
+  return acc;
+}
+
+// Polish the trial point (XN, YN): start from the stored signature `start`
+// (have_start) or from the point's own active set (threshold th), then up to
+// `rounds` primal-dual active-set steps.  Accepts when the KKT check passes
+// at a.tol and then refreshes the scenario's cache entry (a.cache).
+template <class RowDot, class ColDot>
+__device__ __forceinline__ PolishRes polish_wave(const SolveArgs &a, int s, PolishLane d, double XN,
+                                              double YN, double cst, double th, int rounds,
+                                              int have_start, unsigned long long st0,
+                                              unsigned long long st1, unsigned long long st2,
+                                              unsigned long long st3, unsigned long long f0,
+                                              unsigned long long f1, unsigned long long f2,
+                                              unsigned long long f3, double *xs, double *ys,
+                                              double *kkt, int *cpos, RowDot rowdot,
+                                              ColDot coldot) {
+  const int lane = threadIdx.x;
+  const int n = a.n, m = a.m;
+  const double *vs = a.vals_s + (size_t)s * a.nnz;
+  PolishRes res;
+  res.ok = 0;
+  const unsigned long long stv[4] = {st0, st1, st2, st3};
+  ActiveSet as = have_start ? set_from_sig(lane, stv)
+                            : classify_trial(lane, n, m, th, XN, YN, d.L, d.U, d.RL, d.RU);
+  unsigned long long sig[4], prev[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  as.signature(sig);
+  for (int i = 0; i < 4; ++i) res.first[i] = sig[i];
+  if (sig[0] == f0 && sig[1] == f1 && sig[2] == f2 && sig[3] == f3) return res;  // tried already
+  const int Ka = a.cache ? a.K : 0;
+  for (int round = 0; round < rounds; ++round) {
+    as.signature(sig);
+    if (same_sig(sig, prev)) break;  // cycle
+    for (int i = 0; i < 4; ++i) prev[i] = sig[i];
+    const AsSol r = active_set_solve(lane, n, m, as, d.G, d.Q, d.L, d.U, d.RL, d.RU, d.DC, d.kslot,
+                                     Ka, a.P.row_ptr, a.P.col_idx, vs, kkt, cpos, xs);
+    const double XU = r.xu, YU = r.yu;
+    const double xn = lane < n ? clampd(XU, d.L, d.U) : 0.0;
+    const double yn = lane < m ? YU : 0.0;
+    if (lane < n) xs[lane] = xn;
+    if (lane < m) ys[lane] = yn;
+    __syncthreads();
+    const double axn = rowdot();
+    const double aty = coldot();
+    double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    double lam = 0.0;
+    if (lane < n) kkt_terms_col(xn, d.G, d.Q, d.L, d.U, d.DC, aty, lam, v);
+    if (lane < m) kkt_terms_row(axn, yn, d.RL, d.RU, d.DR, v);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = wave_sum(v[i]);
+    double ep, ed, eg, pobj, dobj;
+    kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
+    if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
+      if (a.cache)
+        cache_store(lane, n, m, a, s, r, kkt, XU, YU, d.HL, d.Q, xs, ys, rowdot, coldot);
+      res.ok = 1;
+      res.XN = xn;
+      res.YN = yn;
+      res.AXN = axn;
+      res.pobj = pobj;
+      res.dobj = dobj;
+      res.ep = ep;
+      res.ed = ed;
+      res.eg = eg;
+      return res;
+    }
+    const bool clipped = __ballot(lane < n && XU != xn) != 0ull;
+    double AXU = axn;
+    const double LAMU = lam + d.Q * (XU - xn);
+    __syncthreads();
+    if (clipped) {
+      if (lane < n) xs[lane] = XU;
+      __syncthreads();
+      AXU = rowdot();
+      __syncthreads();
+    }
+    as = classify_pdas(lane, n, m, XU, LAMU, yn, AXU, d.L, d.U, d.RL, d.RU);
+  }
+  return res;
 }
 
 // ------------------------------------------------------------------------
@@ -649,12 +853,9 @@ __device__ void cache_store(int lane, int n, int m, const SolveArgs &c, int s, c
 // P = columns and rows owned per thread, E = extra chunk slots per thread.
 // ------------------------------------------------------------------------
 template <int BLOCK, int P, int E>
-__global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
+__device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, double *lds) {
   constexpr int CPT = P, RPT = P;
   constexpr bool POL = (BLOCK == WAVE && P == 1);  // polish needs lane == line
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int s = blockIdx.x;
-  if (a.done && a.done[s]) return;  // finished by polish_kernel (whole block exits)
   const int T = blockDim.x;
   const int tid = threadIdx.x;
   const int S = a.S, n = a.n, m = a.m;
@@ -829,63 +1030,36 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   // Active-set polish of a PDHG trial point (see active_set_solve).  On
   // success XN/YN/AXN hold the exact point; on failure they are restored.
   unsigned long long pol_first[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-  auto polish_run = [&](double th, int rounds) -> bool {
+  auto polish_run = [&](double th, int rounds, const unsigned long long *start) -> bool {
     if constexpr (!POL) {
       return false;
     } else {
-      const int lane = tid;
-      const double sx = XN[0], sy = YN[0], sa = AXN[0], sl = LAM[0];
       double *kkt = red + MAX_WAVES * 10;
       int *cpos = (int *)(kkt + (size_t)(n + m) * (n + m + 1 + (a.cache ? a.K : 0)));
-      ActiveSet as = classify_trial(lane, n, m, th, XN[0], YN[0], L[0], U[0], RL[0], RU[0]);
-      unsigned long long sig[4], prev[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-      as.signature(sig);
-      if (same_sig(sig, pol_first)) return false;  // this starting set was tried already
-      for (int i = 0; i < 4; ++i) pol_first[i] = sig[i];
-      for (int round = 0; round < rounds; ++round) {
-        as.signature(sig);
-        if (same_sig(sig, prev)) break;  // cycle
-        for (int i = 0; i < 4; ++i) prev[i] = sig[i];
-        const AsSol r = active_set_solve(lane, n, m, as, G[0], Q[0], L[0], U[0], RL[0], RU[0],
-                                         DC[0], kslot, a.cache ? a.K : 0, a.P.row_ptr,
-                                         a.P.col_idx, vs, kkt, cpos, xs);
-        const double XU = r.xu, YU = r.yu;
-        if (lane < m) YN[0] = YU;
-        if (lane < n) XN[0] = clampd(XU, L[0], U[0]);
-        if (lane < n) xs[lane] = XN[0];
-        if (lane < m) ys[lane] = YN[0];
-        __syncthreads();
-        RW.dots(xs, part_r, DOT);
-        if (lane < m) AXN[0] = DOT[0];
-        double v[10];
-        kkt_local(v);
-        v[6] = v[7] = v[8] = v[9] = 0.0;
-        block_sum<10>(v, red);
-        double ep, ed, eg;
-        kkt_measures(v, ep, ed, eg);
-        if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
-          if (a.cache) cache_store(lane, n, m, a, s, r, kkt, XU, YU, HL, Q[0]);
-          return true;
-        }
-        const bool clipped = __ballot(lane < n && XU != XN[0]) != 0ull;
-        double AXU = AXN[0];
-        const double LAMU = LAM[0] + Q[0] * (XU - XN[0]);
-        if (clipped) {
-          __syncthreads();
-          if (lane < n) xs[lane] = XU;
-          __syncthreads();
-          RW.dots(xs, part_r, DOT);
-          AXU = DOT[0];
-        }
-        __syncthreads();
-        as = classify_pdas(lane, n, m, XU, LAMU, YN[0], AXU, L[0], U[0], RL[0], RU[0]);
-      }
-      XN[0] = sx;
-      YN[0] = sy;
-      AXN[0] = sa;
-      LAM[0] = sl;
+      const PolishLane d{G[0], Q[0], L[0], U[0], DC[0], RL[0], RU[0], DR[0], HL, kslot};
+      const bool lane_n = tid < n, lane_m = tid < m;
+      const PolishRes res = polish_wave(
+          a, s, d, XN[0], YN[0], cst, th, rounds, start != nullptr, start ? start[0] : 0ull,
+          start ? start[1] : 0ull, start ? start[2] : 0ull, start ? start[3] : 0ull, pol_first[0],
+          pol_first[1], pol_first[2], pol_first[3], xs, ys, kkt, cpos,
+          [&]() { RW.dots(xs, part_r, DOT); return lane_m ? DOT[0] : 0.0; },
+          [&]() { CL.dots(ys, part_c, DOT); return lane_n ? DOT[0] : 0.0; });
+      for (int i = 0; i < 4; ++i) pol_first[i] = res.first[i];
       __syncthreads();
-      return false;
+      if (!res.ok) {
+        // xs / ys were used as scratch: the PDHG loop rewrites ys before
+        // its next use and xs in its column phase
+        return false;
+      }
+      XN[0] = res.XN;
+      YN[0] = res.YN;
+      AXN[0] = res.AXN;
+      out_pobj = res.pobj;
+      out_dobj = res.dobj;
+      d_ep = res.ep;
+      d_ed = res.ed;
+      d_eg = res.eg;
+      return true;
     }
   };
 
@@ -901,7 +1075,16 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
         YN[b] = Y[b];
         AXN[b] = AX[b];
       }
-      if (polish_run(1e-9, POLISH_ROUNDS)) {
+      // start from the active-set kernel's primal-dual active-set step when
+      // the cached map missed, else from the warm point's active set
+      unsigned long long hs[4];
+      const bool hv = a.hint_ok && a.hint_ok[s];
+      if (hv)
+        for (int i = 0; i < 4; ++i) hs[i] = a.hint[4 * (size_t)s + i];
+      bool ok = false;
+      for (int attempt = hv ? 0 : 1; attempt < 2 && !ok; ++attempt)
+        ok = polish_run(1e-9, POLISH_ROUNDS, attempt == 0 ? hs : nullptr);
+      if (ok) {
         stat = PH_STATUS_OPTIMAL;
         how = 1;
 #pragma unroll
@@ -1015,7 +1198,7 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
       // solve its KKT system; accepted only if the KKT check passes
       const double err = fmax(ep, fmax(ed, eg));
       if (a.polish && err <= POLISH_START) {
-        bool ok = polish_run(fmin(sqrt(err), 1e-3), POLISH_ROUNDS);
+        bool ok = polish_run(fmin(sqrt(err), 1e-3), POLISH_ROUNDS, nullptr);
         if (ok) {
           stat = PH_STATUS_OPTIMAL;
           how = 2;
@@ -1093,6 +1276,25 @@ __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
     a.diag[PH_DIAG_W * s + 3] = d_r;
     a.diag[PH_DIAG_W * s + 4] = (double)how;
   }
+  __syncthreads();  // LDS is reused by the block's next scenario
+}
+
+// PDHG solve kernel: a grid of at most the resident blocks takes scenarios
+// from a work queue (all S, or the work list of scenarios the active-set
+// kernel did not finish); one workgroup owns one scenario at a time.
+template <int BLOCK, int P, int E>
+__global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int next;
+  const int count = a.wl ? *a.wl_count : a.S;
+  for (;;) {
+    if (threadIdx.x == 0) next = atomicAdd(a.queue, 1);
+    __syncthreads();
+    const int idx = next;
+    __syncthreads();
+    if (idx >= count) break;  // every wave of the block leaves here
+    solve_scenario<BLOCK, P, E>(a, a.wl ? a.wl[idx] : idx, lds);
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -1111,92 +1313,121 @@ __device__ __forceinline__ void wsync() {
 }
 
 template <int WPB>
-__global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a, int32_t *done) {
-  __shared__ double sh[WPB][2 * WAVE];
+__global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
+  __shared__ double sh[WPB][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x / WAVE;
   const int s = blockIdx.x * WPB + w;
   if (s >= a.S) return;  // wave-uniform; the kernel has no block barriers
-  const int S = a.S, n = a.n, m = a.m, K = a.K, NM = n + m;
-  double *xs = sh[w];
-  double *ys = sh[w] + WAVE;
-  if (!a.cache_ok[s]) {
-    if (lane == 0) done[s] = 0;
-    return;
-  }
+  const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m);
+  // ---- every load of the scenario is independent of the others: one
+  // round trip to memory (the entry's validity is checked afterwards)
+  const int ok = a.cache_ok[s];
   const double *cs = a.cache + (size_t)s * a.CW;
-  // column state (scaled, as pdhg_kernel)
-  double G = 0.0, Q = 0.0, L = 0.0, U = 0.0, DC = 1.0, HL = 0.0, cstl = 0.0;
-  bool keybad = false;
+  const double *B = cs + K;
+  const double *sb = a.sb + (size_t)s * (4 * n + 3 * m);
+  double DC = 1.0, G = 0.0, L = 0.0, U = 0.0, XU = 0.0, ATY = 0.0;
+  int kslot = -1;
   if (lane < n) {
-    const int j = lane;
-    DC = a.dc[(size_t)s * n + j];
-    double g = a.c[(size_t)j * S + s], q = 0.0;
-    const int k = a.slot_of_col[j];
-    if (k >= 0) {
-      const double W = a.W[(size_t)k * S + s], r = a.rho[(size_t)k * S + s];
-      const double xb = a.xbar[(size_t)k * S + s];
-      HL = a.w_on * W - a.prox_on * r * xb;
-      g += HL;
-      q = a.prox_on * r;
-      cstl = a.prox_on * 0.5 * r * xb * xb;
-    }
-    G = g * DC;
-    Q = q * DC * DC;
-    L = a.l[(size_t)j * S + s] / DC;
-    U = a.u[(size_t)j * S + s] / DC;
-    if (k >= 0) keybad = cs[k] != Q;
+    G = sb[lane];
+    L = sb[n + lane];
+    U = sb[2 * n + lane];
+    DC = sb[3 * n + lane];
+    kslot = a.slot_of_col[lane];
+    XU = B[cv_x(n, m) + lane];
+    ATY = B[cv_aty(n, m) + lane];
   }
-  if (__ballot(keybad)) {  // the entry belongs to another prox term
-    if (lane == 0) done[s] = 0;
+  double DR = 1.0, RL = 0.0, RU = 0.0, YU = 0.0, AX = 0.0;
+  if (lane < m) {
+    RL = sb[4 * n + lane];
+    RU = sb[4 * n + m + lane];
+    DR = sb[4 * n + 2 * m + lane];
+    YU = B[cv_y(n, m) + lane];
+    AX = B[cv_ax(n, m) + lane];
+  }
+  // slot k's PH data at lane k
+  double hk_l = 0.0, qk_l = 0.0, cst_l = 0.0, key_l = 0.0;
+  if (lane < K) {
+    const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
+    const double xb = a.xbar[(size_t)lane * S + s];
+    hk_l = a.w_on * W - a.prox_on * r * xb;
+    qk_l = a.prox_on * r;
+    cst_l = a.prox_on * 0.5 * r * xb * xb;
+    key_l = cs[lane];
+  }
+  // v(h) = base + sum_k h_k D_k, KB slots per batch of independent loads
+  constexpr int KB = 1;
+  for (int k0 = 0; k0 < K; k0 += KB) {
+    double dx[KB], dy[KB], dax[KB], daty[KB];
+#pragma unroll
+    for (int t = 0; t < KB; ++t) {
+      const double *Dk = B + (size_t)(k0 + t + 1) * VL;
+      const bool on = k0 + t < K;
+      dx[t] = (on && lane < n) ? Dk[cv_x(n, m) + lane] : 0.0;
+      daty[t] = (on && lane < n) ? Dk[cv_aty(n, m) + lane] : 0.0;
+      dy[t] = (on && lane < m) ? Dk[cv_y(n, m) + lane] : 0.0;
+      dax[t] = (on && lane < m) ? Dk[cv_ax(n, m) + lane] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < KB; ++t) {
+      const double hk = __shfl(hk_l, (k0 + t) & (WAVE - 1), WAVE);
+      XU = fma(hk, dx[t], XU);
+      ATY = fma(hk, daty[t], ATY);
+      YU = fma(hk, dy[t], YU);
+      AX = fma(hk, dax[t], AX);
+    }
+  }
+  // the slot's h and q moved to its column
+  const double hj = __shfl(hk_l, kslot >= 0 ? kslot : 0, WAVE);
+  const double qj = __shfl(qk_l, kslot >= 0 ? kslot : 0, WAVE);
+  const double keyj = __shfl(key_l, kslot >= 0 ? kslot : 0, WAVE);
+  if (kslot >= 0) G += hj * DC;
+  const double Q = (kslot >= 0 ? qj : 0.0) * DC * DC;
+  // the entry must exist and belong to this prox term
+  if (!ok || __ballot(lane < n && kslot >= 0 && keyj != Q)) {
+    if (lane == 0) {
+      a.hint_ok[s] = 0;
+      a.wl[atomicAdd(a.wl_count, 1)] = s;
+    }
     return;
   }
-  double RL = 0.0, RU = 0.0, DR = 1.0;
-  if (lane < m) {
-    DR = a.dr[(size_t)s * m + lane];
-    RL = a.rl[(size_t)lane * S + s] * DR;
-    RU = a.ru[(size_t)lane * S + s] * DR;
-  }
-  // u(h)
-  double XU = lane < n ? cs[K + lane] : 0.0;
-  double YU = lane < m ? cs[K + n + lane] : 0.0;
-  for (int k = 0; k < K; ++k) {
-    const double hk = __shfl(HL, a.nonant_col[k], WAVE);
-    const double *Dk = cs + K + (size_t)(k + 1) * NM;
-    if (lane < n) XU = fma(hk, Dk[lane], XU);
-    if (lane < m) YU = fma(hk, Dk[n + lane], YU);
-  }
-  const double XN = lane < n ? clampd(XU, L, U) : 0.0;
+  double XN = lane < n ? clampd(XU, L, U) : 0.0;
   const double YN = YU;
-  if (lane < n) xs[lane] = XN;
-  if (lane < m) ys[lane] = YN;
-  wsync();
-  const double *vs = a.vals_s + (size_t)s * a.nnz;
-  double AXN = 0.0, ATY = 0.0;
-  if (lane < m)
-    for (int p = a.P.row_ptr[lane]; p < a.P.row_ptr[lane + 1]; ++p)
-      AXN = fma(vs[p], xs[a.P.col_idx[p]], AXN);
-  if (lane < n)
-    for (int p = a.P.col_ptr[lane]; p < a.P.col_ptr[lane + 1]; ++p)
-      ATY = fma(vs[a.P.csc_k[p]], ys[a.P.csc_row[p]], ATY);
+  double AXN = AX;
+  double ATYN = ATY;
+  if (__ballot(lane < n && XN != XU)) {
+    // a column left its bounds: the products of the clipped point by SpMV
+    double *xs = sh[w];
+    if (lane < n) xs[lane] = XN;
+    wsync();
+    AXN = pat_rowdot(lane, m, a.P, a.vals_s + (size_t)s * a.nnz, xs);
+  }
   double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  double lam;
-  if (lane < n) kkt_terms_col(XN, G, Q, L, U, DC, ATY, lam, v);
+  double lam = 0.0;
+  if (lane < n) kkt_terms_col(XN, G, Q, L, U, DC, ATYN, lam, v);
   if (lane < m) kkt_terms_row(AXN, YN, RL, RU, DR, v);
 #pragma unroll
   for (int i = 0; i < 6; ++i) v[i] = wave_sum(v[i]);
-  const double cst = wave_sum(cstl);
+  const double cst = wave_sum(cst_l);
   double ep, ed, eg, pobj, dobj;
   kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
-  const bool ok = ep <= a.tol && ed <= a.tol && eg <= a.tol;
-  if (!ok) {
-    if (lane == 0) done[s] = 0;
+  if (!(ep <= a.tol && ed <= a.tol && eg <= a.tol)) {
+    // the active set moved: hand pdhg_kernel the primal-dual active-set
+    // step from the map's (unclipped) point as the polish's first guess
+    const double lamu = Q * XU + G - ATY;
+    const ActiveSet as = classify_pdas(lane, n, m, XU, lamu, YU, AX, L, U, RL, RU);
+    unsigned long long sig[4];
+    as.signature(sig);
+    if (lane < 4) a.hint[4 * (size_t)s + lane] = sig[lane];
+    if (lane == 0) {
+      a.hint_ok[s] = 1;
+      a.wl[atomicAdd(a.wl_count, 1)] = s;
+    }
     return;
   }
   if (lane < n) a.x[(size_t)lane * S + s] = XN * DC;
   if (lane < m) a.y[(size_t)lane * S + s] = YN * DR;
   if (lane == 0) {
-    done[s] = 1;
     a.status[s] = PH_STATUS_OPTIMAL;
     a.iters[s] = 0;
     a.pobj[s] = pobj;
@@ -1352,7 +1583,12 @@ struct ph_batch {
   // active-set cache (polish-size scenarios): [S][CW] doubles + flags
   int CW = 0;
   double *d_cache = nullptr;
-  int32_t *d_cache_ok = nullptr, *d_done = nullptr;
+  int32_t *d_cache_ok = nullptr;
+  unsigned long long *d_hint = nullptr;
+  int32_t *d_hint_ok = nullptr, *d_wl = nullptr;
+  int32_t *d_ctr = nullptr;  // [2]: work-list count, work-queue counter
+  double *d_sb = nullptr;    // [S][4n+3m] static block (polish-size scenarios)
+  int pdhg_grid = 0;         // resident blocks of the pdhg kernel (0: not yet known)
   // extra chunks of lines longer than LINE_D (see LineRegs)
   int xr = 0, xc = 0;
   int32_t *d_r_pb = nullptr, *d_r_pos = nullptr, *d_r_len = nullptr;
@@ -1481,7 +1717,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
       (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
-      (rc = dalloc(&b->d_summary, 4)) ||
+      (rc = dalloc(&b->d_summary, 4)) || (rc = dalloc(&b->d_ctr, 2)) ||
       (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
@@ -1556,6 +1792,16 @@ int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const doubl
                        b->S, b->n, b->m, b->nnz, P, vals, b->d_vals_s, b->d_dr, b->d_dc, b->d_eta);
   });
   HIP_OK(hipGetLastError());
+  if (polish_fits(b)) {
+    if (!b->d_sb) {
+      int rc = dalloc(&b->d_sb, (size_t)b->S * (4 * b->n + 3 * b->m));
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(static_block_kernel, dim3((b->S + 3) / 4), dim3(256), 0, b->stream, b->S,
+                       b->n, b->m, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_dc, b->d_dr,
+                       b->d_sb);
+    HIP_OK(hipGetLastError());
+  }
   b->bound = true;
   return PH_OK;
 }
@@ -1576,15 +1822,19 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
   HIP_OK(hipMemcpyAsync(b->d_slot_of_col, slot.data(), sizeof(int32_t) * b->n, hipMemcpyHostToDevice, b->stream));
   b->K = K;
   // active-set cache for scenarios the one-wave polish covers
-  for (void *p : {(void *)b->d_cache, (void *)b->d_cache_ok, (void *)b->d_done})
+  for (void *p : {(void *)b->d_cache, (void *)b->d_cache_ok, (void *)b->d_hint,
+                  (void *)b->d_hint_ok, (void *)b->d_wl})
     if (p) (void)hipFree(p);
   b->d_cache = nullptr;
-  b->d_cache_ok = b->d_done = nullptr;
+  b->d_cache_ok = b->d_hint_ok = b->d_wl = nullptr;
+  b->d_hint = nullptr;
   b->CW = 0;
+  b->pdhg_grid = 0;  // LDS per block depends on the cache
   if (polish_fits(b)) {
-    b->CW = K + (K + 1) * (b->n + b->m);
+    b->CW = K + (K + 1) * 2 * (b->n + b->m);
     if ((rc = dalloc(&b->d_cache, (size_t)b->S * b->CW)) || (rc = dalloc(&b->d_cache_ok, b->S)) ||
-        (rc = dalloc(&b->d_done, b->S)))
+        (rc = dalloc(&b->d_hint, (size_t)b->S * 4)) || (rc = dalloc(&b->d_hint_ok, b->S)) ||
+        (rc = dalloc(&b->d_wl, b->S)))
       return rc;
     HIP_OK(hipMemsetAsync(b->d_cache_ok, 0, sizeof(int32_t) * b->S, b->stream));
   }
@@ -1619,21 +1869,39 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.K = b->K;
   a.CW = b->CW;
   a.nonant_col = b->d_nonant_col;
-  a.cache = a.polish ? b->d_cache : nullptr;
+  a.cache = (a.polish && b->d_sb) ? b->d_cache : nullptr;
+  a.sb = b->d_sb;
   a.cache_ok = b->d_cache_ok;
-  a.done = nullptr;
+  a.hint = nullptr;
+  a.hint_ok = nullptr;
+  a.wl = nullptr;
+  a.wl_count = b->d_ctr;
+  a.queue = b->d_ctr + 1;
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
+  if (b->pdhg_grid == 0) {
+    int per_cu = 0, cus = 0, dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    DISPATCH_GEOM(b->block, b->per, b->ext, {
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pdhg_kernel<B_, P_, E_>, B_, lds));
+    });
+    b->pdhg_grid = std::max(1, per_cu) * std::max(1, cus);
+  }
+  HIP_OK(hipMemsetAsync(b->d_ctr, 0, 2 * sizeof(int32_t), b->stream));
   if (a.cache && a.warm) {
+    a.hint = b->d_hint;
+    a.hint_ok = b->d_hint_ok;
+    a.wl = b->d_wl;
     constexpr int WPB = 4;
     hipLaunchKernelGGL((active_set_kernel<WPB>), dim3((b->S + WPB - 1) / WPB), dim3(WPB * WAVE),
-                       0, b->stream, a, b->d_done);
+                       0, b->stream, a);
     HIP_OK(hipGetLastError());
-    a.done = b->d_done;
   }
+  const int grid = std::min(b->S, b->pdhg_grid);
   DISPATCH_GEOM(b->block, b->per, b->ext, {
-    hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(b->S), dim3(B_), lds, b->stream, a);
+    hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(grid), dim3(B_), lds, b->stream, a);
   });
   HIP_OK(hipGetLastError());
   hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(1024), 0, b->stream, b->S, status, iters,
@@ -1711,7 +1979,7 @@ void ph_batch_destroy(ph_batch_t b) {
   void *ptrs[] = {b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k,
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
-                  b->d_cache, b->d_cache_ok, b->d_done,
+                  b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_ctr, b->d_sb,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
