@@ -178,6 +178,57 @@ int ph_batch_get_diag(ph_batch_t b, double *out /*host [S][PH_DIAG_W]*/);
  */
 int ph_batch_solve_summary(ph_batch_t b, int64_t *out /*host [4]*/);
 
+/*
+ * Device-side PH iteration control (iterk_loop without a host round trip
+ * per iteration, phbase.py:1498-1553).  While the loop is enabled, every
+ * per-iteration kernel (ph_xbar_accum, ph_update_w, ph_segment_sum,
+ * ph_pdhg_solve and the convergence kernels) first reads the batch's stop
+ * flag and does nothing once it is set, so the host can queue (or replay as
+ * a HIP graph) many iterations and look at the flag only now and then.
+ * One iteration, in the reference's order:
+ *   [allreduce of the Compute_Xbar sums]       (multi-rank only)
+ *   ph_update_w (with W)                       Compute_Xbar broadcast + Update_W
+ *   ph_loop_conv_local                         convergence_diff (one rank), or
+ *   ph_segment_sum + [allreduce] + ph_loop_conv  (several ranks):
+ *       conv = sum_r parts[r]/cnt[r] / nproc (phbase.py:254-276) into
+ *       conv_hist[iter-1]; stop (1) when conv < convthresh, BEFORE this
+ *       iteration's solve (x stays stale, as in the reference)
+ *   ph_pdhg_solve                              solve_loop; its post-solve
+ *       kernel also computes the next iteration's Compute_Xbar sums (when
+ *       ph_loop_set_xbar gave them) and begins the next iteration
+ *       (counter += 1, or stop (2) past iter_limit)
+ * ph_loop_reset sets iter = start_iter, clears the flag and the solve
+ * counters and begins iteration start_iter + 1; before the first pass the
+ * host computes the Compute_Xbar sums once (ph_xbar_accum).  ph_loop_enable
+ * switches the flag checks on / off; ph_loop_status copies {stop, iter,
+ * not-optimal solves, solves, PDHG iterations (sum), PDHG iterations (max),
+ * polished} to host out[7] (synchronises).
+ */
+int ph_loop_reset(ph_batch_t b, int32_t start_iter, int32_t iter_limit,
+                  double convthresh);
+int ph_loop_enable(ph_batch_t b, int32_t on);
+int ph_loop_set_xbar(ph_batch_t b, const double *x, const double *prob_coeff,
+                     int32_t G, const int32_t *slot_k, const int32_t *slot_s0,
+                     const int32_t *slot_s1, double *out_sums);
+int ph_loop_conv(ph_batch_t b, const double *parts /*dev [R]*/,
+                 const double *cnt /*dev [R]*/, int32_t R, double nproc,
+                 double *conv_hist /*dev [iter_limit]*/);
+int ph_loop_conv_local(ph_batch_t b, const double *absdiff /*dev [S]*/,
+                       const int32_t *seg /*dev [R+1]*/, int32_t R,
+                       const double *cnt /*dev [R]*/, double nproc,
+                       double *parts /*dev [R] out*/, double *conv_hist);
+int ph_loop_status(ph_batch_t b, int64_t *out /*host [7]*/);
+
+/*
+ * Kernel timing of ph_pdhg_solve with HIP events recorded on the batch's
+ * stream around the active-set kernel and the PDHG kernel of every solve
+ * while timing is on (set_timing clears the record).  read_timing
+ * synchronises and returns out[3] = {solves recorded, total active-set
+ * kernel ms, total PDHG kernel ms}.  (Measurement support; bench.py.)
+ */
+int ph_batch_set_timing(ph_batch_t b, int32_t on);
+int ph_batch_read_timing(ph_batch_t b, double *out /*host [3]*/);
+
 /* Block until all work queued on the batch's stream has finished. */
 int ph_batch_sync(ph_batch_t b);
 

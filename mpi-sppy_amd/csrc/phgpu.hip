@@ -253,6 +253,22 @@ __global__ void __launch_bounds__(256) static_block_kernel(
   }
 }
 
+// ------------------------------------------------------------------------
+// Device-side PH loop control (see ph_loop_* in phgpu.h).
+// ------------------------------------------------------------------------
+struct LoopCtl {
+  int32_t stop;   // 0 running, 1 converged, 2 iteration limit
+  int32_t iter;   // PH iteration of the current pass (1-based)
+  int32_t limit;  // PHIterLimit
+  int32_t pad;
+  double thresh;  // convthresh
+  unsigned long long acc[5];  // not optimal, solves, iters sum, iters max, polished
+};
+
+__device__ __forceinline__ bool stopped(const LoopCtl *c) {
+  return c && *(volatile const int32_t *)&c->stop;
+}
+
 struct SolveArgs {
   int S, n, m, nnz;
   Pattern P;
@@ -284,6 +300,7 @@ struct SolveArgs {
   // scenarios for pdhg_kernel: wl == null -> all S, else wl[0 .. *wl_count)
   int32_t *wl, *wl_count;
   int32_t *queue;  // work-queue counter (0 at launch)
+  const LoopCtl *ctl;  // device loop control or null
 };
 
 // Active-set polish: largest KKT system (free columns + active rows) and the
@@ -1286,14 +1303,16 @@ template <int BLOCK, int P, int E>
 __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int next;
-  const int count = a.wl ? *a.wl_count : a.S;
-  for (;;) {
-    if (threadIdx.x == 0) next = atomicAdd(a.queue, 1);
-    __syncthreads();
-    const int idx = next;
-    __syncthreads();
-    if (idx >= count) break;  // every wave of the block leaves here
+  const int count = stopped(a.ctl) ? 0 : (a.wl ? *a.wl_count : a.S);
+  // first scenario by block index (no atomics while the list is short),
+  // then from the queue
+  int idx = blockIdx.x;
+  while (idx < count) {  // uniform over the block
     solve_scenario<BLOCK, P, E>(a, a.wl ? a.wl[idx] : idx, lds);
+    if (threadIdx.x == 0) next = (int)gridDim.x + atomicAdd(a.queue, 1);
+    __syncthreads();
+    idx = next;
+    __syncthreads();
   }
 }
 
@@ -1318,7 +1337,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x / WAVE;
   const int s = blockIdx.x * WPB + w;
-  if (s >= a.S) return;  // wave-uniform; the kernel has no block barriers
+  if (s >= a.S || stopped(a.ctl)) return;  // wave-uniform; no block barriers
   const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m);
   // ---- every load of the scenario is independent of the others: one
   // round trip to memory (the entry's validity is checked afterwards)
@@ -1441,30 +1460,85 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   }
 }
 
+// Start the next iteration (phbase.py:1498 loop head): count it, or stop
+// past the limit.  Called by one thread at the end of an iteration.
+__device__ __forceinline__ void loop_advance(LoopCtl *c) {
+  if (c->stop) return;
+  if (c->iter >= c->limit) c->stop = 2;
+  else c->iter += 1;
+}
+
+// conv = (sum_r parts[r]/cnt[r]) / nproc, summed in rank order like the host
+// (also clears the solve's work-list counters `ctr` for this iteration)
+__global__ void loop_conv_kernel(LoopCtl *c, const double *__restrict__ parts,
+                                 const double *__restrict__ cnt, int R, double nproc,
+                                 double *__restrict__ hist, int32_t *ctr) {
+  if (c->stop) return;
+  double v = 0.0;
+  for (int r = 0; r < R; ++r) v += parts[r] / cnt[r];
+  v /= nproc;
+  hist[c->iter - 1] = v;
+  if (v < c->thresh) c->stop = 1;
+  ctr[0] = 0;
+  ctr[1] = 0;
+}
+
+// Single-rank form: the per-reference-rank sums of absdiff over the
+// segments and the conv test in one block (deterministic order).
+__global__ void __launch_bounds__(1024) loop_conv_local_kernel(
+    LoopCtl *c, const double *__restrict__ v, const int32_t *__restrict__ seg, int R,
+    const double *__restrict__ cnt, double nproc, double *__restrict__ parts,
+    double *__restrict__ hist, int32_t *ctr) {
+  __shared__ double red[MAX_WAVES];
+  if (stopped(c)) return;
+  double conv = 0.0;
+  for (int r = 0; r < R; ++r) {
+    double acc[1] = {0.0};
+    for (int s = seg[r] + threadIdx.x; s < seg[r + 1]; s += blockDim.x) acc[0] += v[s];
+    block_sum<1>(acc, red);
+    if (threadIdx.x == 0) parts[r] = acc[0];
+    conv += acc[0] / cnt[r];
+  }
+  if (threadIdx.x == 0) {
+    conv /= nproc;
+    hist[c->iter - 1] = conv;
+    if (conv < c->thresh) c->stop = 1;
+    ctr[0] = 0;
+    ctr[1] = 0;
+  }
+}
+
 // ------------------------------------------------------------------------
 // nonanticipativity kernels (scenario-fastest, coalesced)
 // ------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) xbar_accum_kernel(
-    int S, const double *__restrict__ x, const double *__restrict__ pc,
-    const int32_t *__restrict__ nonant_col, const int32_t *__restrict__ slot_k,
-    const int32_t *__restrict__ s0, const int32_t *__restrict__ s1, int G,
-    double *__restrict__ out) {
+struct XbarArgs {  // Compute_Xbar's weighted sums (see ph_xbar_accum)
+  int S, G;
+  const double *x, *pc;
+  const int32_t *nonant_col, *slot_k, *s0, *s1;
+  double *out;  // [2G]
+};
+
+__device__ __forceinline__ void xbar_sums_block(const XbarArgs &xa, int g) {
   __shared__ double red[MAX_WAVES * 2];
-  const int g = blockIdx.x;
-  const int k = slot_k[g];
-  const double *xr = x + (size_t)nonant_col[k] * S;
-  const double *pr = pc + (size_t)k * S;
+  const int k = xa.slot_k[g];
+  const double *xr = xa.x + (size_t)xa.nonant_col[k] * xa.S;
+  const double *pr = xa.pc + (size_t)k * xa.S;
   double v[2] = {0.0, 0.0};
-  for (int s = s0[g] + threadIdx.x; s < s1[g]; s += blockDim.x) {
-    double xv = xr[s], p = pr[s];
+  for (int s = xa.s0[g] + threadIdx.x; s < xa.s1[g]; s += blockDim.x) {
+    const double xv = xr[s], p = pr[s];
     v[0] += p * xv;
     v[1] += p * xv * xv;
   }
   block_sum<2>(v, red);
   if (threadIdx.x == 0) {
-    out[g] = v[0];
-    out[G + g] = v[1];
+    xa.out[g] = v[0];
+    xa.out[xa.G + g] = v[1];
   }
+}
+
+__global__ void __launch_bounds__(1024) xbar_accum_kernel(XbarArgs xa, const LoopCtl *ctl) {
+  if (stopped(ctl)) return;
+  xbar_sums_block(xa, blockIdx.x);
 }
 
 __global__ void __launch_bounds__(256) update_w_kernel(
@@ -1472,9 +1546,9 @@ __global__ void __launch_bounds__(256) update_w_kernel(
     const double *__restrict__ sums, int G, const int32_t *__restrict__ gid,
     const double *__restrict__ rho, const double *__restrict__ wc,
     double *__restrict__ xbar, double *__restrict__ xsqbar, double *__restrict__ W,
-    double *__restrict__ absdiff) {
+    double *__restrict__ absdiff, const LoopCtl *ctl) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= S) return;
+  if (s >= S || stopped(ctl)) return;
   double acc = 0.0;
   for (int k = 0; k < K; ++k) {
     const size_t o = (size_t)k * S + s;
@@ -1496,8 +1570,9 @@ __global__ void __launch_bounds__(256) update_w_kernel(
 
 __global__ void __launch_bounds__(1024) segment_sum_kernel(
     const double *__restrict__ v, const double *__restrict__ w,
-    const int32_t *__restrict__ seg, double *__restrict__ out) {
+    const int32_t *__restrict__ seg, double *__restrict__ out, const LoopCtl *ctl) {
   __shared__ double red[MAX_WAVES];
+  if (stopped(ctl)) return;
   const int r = blockIdx.x;
   double acc[1] = {0.0};
   for (int s = seg[r] + threadIdx.x; s < seg[r + 1]; s += blockDim.x)
@@ -1512,8 +1587,14 @@ __global__ void __launch_bounds__(1024) segment_sum_kernel(
 __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__restrict__ status,
                                                        const int32_t *__restrict__ iters,
                                                        const double *__restrict__ diag,
-                                                       unsigned long long *__restrict__ out) {
+                                                       unsigned long long *__restrict__ out,
+                                                       LoopCtl *ctl, XbarArgs xa) {
   __shared__ unsigned long long red[4][MAX_WAVES];
+  if (stopped(ctl)) return;
+  if (blockIdx.x > 0) {  // device loop: next iteration's Compute_Xbar sums
+    xbar_sums_block(xa, blockIdx.x - 1);
+    return;
+  }
   unsigned long long v[4] = {0ull, 0ull, 0ull, 0ull};
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
     const unsigned long long it = (unsigned long long)iters[s];
@@ -1540,6 +1621,14 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
       unsigned long long t = red[i][0];
       for (int w = 1; w < nw; ++w) t = i == 2 ? (red[i][w] > t ? red[i][w] : t) : t + red[i][w];
       out[i] = t;
+    }
+    if (ctl) {  // running totals of the device loop, then the next iteration
+      ctl->acc[0] += out[0];
+      ctl->acc[1] += (unsigned long long)S;
+      ctl->acc[2] += out[1];
+      ctl->acc[3] = out[2] > ctl->acc[3] ? out[2] : ctl->acc[3];
+      ctl->acc[4] += out[3];
+      loop_advance(ctl);
     }
   }
 }
@@ -1588,6 +1677,13 @@ struct ph_batch {
   int32_t *d_hint_ok = nullptr, *d_wl = nullptr;
   int32_t *d_ctr = nullptr;  // [2]: work-list count, work-queue counter
   double *d_sb = nullptr;    // [S][4n+3m] static block (polish-size scenarios)
+  LoopCtl *d_ctl = nullptr;  // device loop control
+  bool loop_on = false;
+  XbarArgs loop_xa{};         // Compute_Xbar sums done by the post-solve kernel (G > 0)
+  // optional per-kernel timing of ph_pdhg_solve (HIP events on the stream)
+  bool timing = false;
+  std::vector<hipEvent_t> ev;  // 4 per recorded solve: as0, as1 (=pd0), pd1, spare
+  size_t ev_used = 0;
   int pdhg_grid = 0;         // resident blocks of the pdhg kernel (0: not yet known)
   // extra chunks of lines longer than LINE_D (see LineRegs)
   int xr = 0, xc = 0;
@@ -1668,6 +1764,8 @@ void build_chunks(int lines, const std::vector<int32_t> &ptr, std::vector<int32_
 
 }  // namespace
 
+static LoopCtl *loop_ctl(const ph_batch *b) { return b->loop_on ? b->d_ctl : nullptr; }
+
 extern "C" {
 
 const char *ph_version(void) { return PHGPU_VERSION; }
@@ -1717,7 +1815,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
       (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
-      (rc = dalloc(&b->d_summary, 4)) || (rc = dalloc(&b->d_ctr, 2)) ||
+      (rc = dalloc(&b->d_summary, 4)) || (rc = dalloc(&b->d_ctr, 2)) || (rc = dalloc(&b->d_ctl, 1)) ||
       (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
@@ -1877,6 +1975,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.wl = nullptr;
   a.wl_count = b->d_ctr;
   a.queue = b->d_ctr + 1;
+  a.ctl = loop_ctl(b);
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
@@ -1889,7 +1988,21 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     });
     b->pdhg_grid = std::max(1, per_cu) * std::max(1, cus);
   }
-  HIP_OK(hipMemsetAsync(b->d_ctr, 0, 2 * sizeof(int32_t), b->stream));
+  // (in the device loop the convergence kernel has cleared the counters)
+  if (!b->loop_on) HIP_OK(hipMemsetAsync(b->d_ctr, 0, 2 * sizeof(int32_t), b->stream));
+  hipEvent_t *tev = nullptr;
+  if (b->timing) {
+    if (b->ev_used + 3 > b->ev.size()) {
+      for (int i = 0; i < 3; ++i) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreate(&e));
+        b->ev.push_back(e);
+      }
+    }
+    tev = &b->ev[b->ev_used];
+    b->ev_used += 3;
+    HIP_OK(hipEventRecord(tev[0], b->stream));
+  }
   if (a.cache && a.warm) {
     a.hint = b->d_hint;
     a.hint_ok = b->d_hint_ok;
@@ -1899,13 +2012,18 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
                        0, b->stream, a);
     HIP_OK(hipGetLastError());
   }
+  if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
   const int grid = std::min(b->S, b->pdhg_grid);
   DISPATCH_GEOM(b->block, b->per, b->ext, {
     hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(grid), dim3(B_), lds, b->stream, a);
   });
   HIP_OK(hipGetLastError());
-  hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(1024), 0, b->stream, b->S, status, iters,
-                     b->d_diag, b->d_summary);
+  if (tev) HIP_OK(hipEventRecord(tev[2], b->stream));
+  // device loop: the summary block also advances the iteration, and G
+  // more blocks compute the next iteration's Compute_Xbar sums
+  const int post_g = (b->loop_on && b->loop_xa.x == x) ? b->loop_xa.G : 0;
+  hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, status,
+                     iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -1916,8 +2034,8 @@ int ph_xbar_accum(ph_batch_t b, const double *x, const double *prob_coeff, int32
   if (!b || !x || !prob_coeff || G <= 0 || !slot_k || !slot_s0 || !slot_s1 || !out_sums)
     return fail(PH_EINVAL, "ph_xbar_accum: bad arguments");
   if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_xbar_accum: no nonants declared");
-  hipLaunchKernelGGL(xbar_accum_kernel, dim3(G), dim3(1024), 0, b->stream, b->S, x, prob_coeff,
-                     b->d_nonant_col, slot_k, slot_s0, slot_s1, G, out_sums);
+  const XbarArgs xa{b->S, G, x, prob_coeff, b->d_nonant_col, slot_k, slot_s0, slot_s1, out_sums};
+  hipLaunchKernelGGL(xbar_accum_kernel, dim3(G), dim3(1024), 0, b->stream, xa, loop_ctl(b));
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -1929,7 +2047,8 @@ int ph_update_w(ph_batch_t b, const double *x, const double *sums, int32_t G, co
     return fail(PH_EINVAL, "ph_update_w: bad arguments");
   if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_update_w: no nonants declared");
   hipLaunchKernelGGL(update_w_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->S,
-                     b->K, x, b->d_nonant_col, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff);
+                     b->K, x, b->d_nonant_col, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff,
+                     loop_ctl(b));
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -1937,7 +2056,8 @@ int ph_update_w(ph_batch_t b, const double *x, const double *sums, int32_t G, co
 int ph_segment_sum(ph_batch_t b, const double *v, const double *w, int32_t R, const int32_t *seg,
                    double *out) {
   if (!b || !v || R <= 0 || !seg || !out) return fail(PH_EINVAL, "ph_segment_sum: bad arguments");
-  hipLaunchKernelGGL(segment_sum_kernel, dim3(R), dim3(1024), 0, b->stream, v, w, seg, out);
+  hipLaunchKernelGGL(segment_sum_kernel, dim3(R), dim3(1024), 0, b->stream, v, w, seg, out,
+                     loop_ctl(b));
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -1968,6 +2088,103 @@ int ph_batch_solve_summary(ph_batch_t b, int64_t *out) {
   return PH_OK;
 }
 
+int ph_loop_reset(ph_batch_t b, int32_t start_iter, int32_t iter_limit, double convthresh) {
+  if (!b || start_iter < 0 || iter_limit < 0) return fail(PH_EINVAL, "ph_loop_reset: bad arguments");
+  LoopCtl h;
+  std::memset(&h, 0, sizeof(h));
+  h.iter = start_iter;
+  h.limit = iter_limit;
+  h.thresh = convthresh;
+  // begin the first iteration (the post-solve kernel begins the others)
+  if (h.iter >= h.limit) h.stop = 2;
+  else h.iter += 1;
+  HIP_OK(hipMemcpyAsync(b->d_ctl, &h, sizeof(h), hipMemcpyHostToDevice, b->stream));
+  HIP_OK(hipStreamSynchronize(b->stream));  // h is on this stack frame
+  return PH_OK;
+}
+
+int ph_loop_enable(ph_batch_t b, int32_t on) {
+  if (!b) return fail(PH_EINVAL, "null batch");
+  b->loop_on = on != 0;
+  return PH_OK;
+}
+
+int ph_loop_set_xbar(ph_batch_t b, const double *x, const double *prob_coeff, int32_t G,
+                     const int32_t *slot_k, const int32_t *slot_s0, const int32_t *slot_s1,
+                     double *out_sums) {
+  if (!b) return fail(PH_EINVAL, "null batch");
+  if (G <= 0) {
+    b->loop_xa = XbarArgs{};
+    return PH_OK;
+  }
+  if (!x || !prob_coeff || !slot_k || !slot_s0 || !slot_s1 || !out_sums || !b->d_nonant_col)
+    return fail(PH_EINVAL, "ph_loop_set_xbar: bad arguments");
+  b->loop_xa = XbarArgs{b->S, G, x, prob_coeff, b->d_nonant_col, slot_k, slot_s0, slot_s1, out_sums};
+  return PH_OK;
+}
+
+int ph_loop_conv(ph_batch_t b, const double *parts, const double *cnt, int32_t R, double nproc,
+                 double *conv_hist) {
+  if (!b || !b->loop_on || !parts || !cnt || R <= 0 || !conv_hist)
+    return fail(PH_EINVAL, "ph_loop_conv: bad arguments (or loop not enabled)");
+  if (!(nproc > 0.0)) return fail(PH_EINVAL, "ph_loop_conv: nproc must be > 0");
+  hipLaunchKernelGGL(loop_conv_kernel, dim3(1), dim3(1), 0, b->stream, b->d_ctl, parts, cnt, R,
+                     nproc, conv_hist, b->d_ctr);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_loop_conv_local(ph_batch_t b, const double *absdiff, const int32_t *seg, int32_t R,
+                       const double *cnt, double nproc, double *parts, double *conv_hist) {
+  if (!b || !b->loop_on || !absdiff || !seg || R <= 0 || !cnt || !parts || !conv_hist)
+    return fail(PH_EINVAL, "ph_loop_conv_local: bad arguments (or loop not enabled)");
+  if (!(nproc > 0.0)) return fail(PH_EINVAL, "ph_loop_conv_local: nproc must be > 0");
+  hipLaunchKernelGGL(loop_conv_local_kernel, dim3(1), dim3(1024), 0, b->stream, b->d_ctl, absdiff,
+                     seg, R, cnt, nproc, parts, conv_hist, b->d_ctr);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_loop_status(ph_batch_t b, int64_t *out) {
+  if (!b || !out) return fail(PH_EINVAL, "ph_loop_status: bad arguments");
+  LoopCtl h;
+  HIP_OK(hipMemcpyAsync(&h, b->d_ctl, sizeof(h), hipMemcpyDeviceToHost, b->stream));
+  HIP_OK(hipStreamSynchronize(b->stream));
+  out[0] = h.stop;
+  out[1] = h.iter;
+  out[2] = (int64_t)h.acc[0];
+  out[3] = (int64_t)h.acc[1];
+  out[4] = (int64_t)h.acc[2];
+  out[5] = (int64_t)h.acc[3];
+  out[6] = (int64_t)h.acc[4];
+  return PH_OK;
+}
+
+int ph_batch_set_timing(ph_batch_t b, int32_t on) {
+  if (!b) return fail(PH_EINVAL, "null batch");
+  b->timing = on != 0;
+  b->ev_used = 0;
+  return PH_OK;
+}
+
+int ph_batch_read_timing(ph_batch_t b, double *out) {
+  if (!b || !out) return fail(PH_EINVAL, "ph_batch_read_timing: bad arguments");
+  HIP_OK(hipStreamSynchronize(b->stream));
+  double t_as = 0.0, t_pd = 0.0;
+  const size_t n = b->ev_used / 3;
+  for (size_t i = 0; i < n; ++i) {
+    float ms0 = 0.f, ms1 = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms0, b->ev[3 * i], b->ev[3 * i + 1]));
+    HIP_OK(hipEventElapsedTime(&ms1, b->ev[3 * i + 1], b->ev[3 * i + 2]));
+    t_as += ms0;
+    t_pd += ms1;
+  }
+  out[0] = (double)n;
+  out[1] = t_as;
+  out[2] = t_pd;
+  return PH_OK;
+}
+
 int ph_batch_sync(ph_batch_t b) {
   if (!b) return fail(PH_EINVAL, "null batch");
   HIP_OK(hipStreamSynchronize(b->stream));
@@ -1980,9 +2197,11 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_ctr, b->d_sb,
+                  b->d_ctl,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  for (hipEvent_t e : b->ev) (void)hipEventDestroy(e);
   delete b;
 }
 

@@ -48,6 +48,15 @@ SIGNATURES = [
     ("ph_eval_objective", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_dbl, _c_dbl, _c_ptr]),
     ("ph_batch_get_diag", _c_int, [_c_ptr, _c_ptr]),
     ("ph_batch_solve_summary", _c_int, [_c_ptr, _c_ptr]),
+    ("ph_loop_reset", _c_int, [_c_ptr, _c_int, _c_int, _c_dbl]),
+    ("ph_loop_enable", _c_int, [_c_ptr, _c_int]),
+    ("ph_loop_set_xbar", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_int, _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
+    ("ph_loop_conv", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_int, _c_dbl, _c_ptr]),
+    ("ph_loop_conv_local", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_int, _c_ptr, _c_dbl, _c_ptr,
+                                    _c_ptr]),
+    ("ph_loop_status", _c_int, [_c_ptr, _c_ptr]),
+    ("ph_batch_set_timing", _c_int, [_c_ptr, _c_int]),
+    ("ph_batch_read_timing", _c_int, [_c_ptr, _c_ptr]),
     ("ph_batch_sync", _c_int, [_c_ptr]),
     ("ph_batch_destroy", None, [_c_ptr]),
 ]

@@ -8,6 +8,8 @@ Maximize models are turned into min form here (c -> -c), exactly the sign
 convention of ``phbase.py:1206-1209`` (``objfct.expr -= ph_term``): the PH
 terms are then always *added* in min form.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -162,10 +164,12 @@ class DeviceBatch:
         self.rl = up(data.rl) if self.m else torch.zeros(1, **f64)
         self.ru = up(data.ru) if self.m else torch.zeros(1, **f64)
         h = _native._c_ptr()
+        sh = _native.stream_handle(stream)
+        self._stream_handle = sh.value or 0
         _native.check(lib.ph_batch_create(h, self.S, self.n, self.m, self.nnz,
                                           data.row_ptr.ctypes.data_as(_native._c_ptr),
                                           data.col_idx.ctypes.data_as(_native._c_ptr),
-                                          _native.stream_handle(stream)), "ph_batch_create")
+                                          sh), "ph_batch_create")
         self.handle = h
         _native.check(lib.ph_batch_bind(h, _native.ptr(vals), _native.ptr(self.c),
                                         _native.ptr(self.l), _native.ptr(self.u),
@@ -188,6 +192,7 @@ class DeviceBatch:
         self._summary = np.zeros(4, dtype=np.int64)
         self.time_kernel = False  # record HIP events around each solve launch
         self._events = None
+        self.event_log = []       # every (start, end) event pair recorded
 
     def solve(self, W, rho, xbar, w_on, prox_on, tol=1e-9, max_iters=200000,
               check_every=64, warm_start=True, reflection=1.0, polish=True):
@@ -197,6 +202,7 @@ class DeviceBatch:
             stream = torch.cuda.current_stream(self.dev) if self.stream is None else self.stream
             self._events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self._events[0].record(stream)
+            self.event_log.append(self._events)
         _native.check(self.lib.ph_pdhg_solve(
             self.handle, _native.ptr(W), _native.ptr(rho), _native.ptr(xbar),
             float(w_on), float(prox_on), _native.ptr(self.x), _native.ptr(self.y),
@@ -211,12 +217,75 @@ class DeviceBatch:
             return None
         return self._events[0].elapsed_time(self._events[1])
 
+    def set_timing(self, on):
+        """Record HIP events around the active-set and PDHG kernels of every
+        solve (library side, on the launch stream)."""
+        _native.check(self.lib.ph_batch_set_timing(self.handle, 1 if on else 0),
+                      "ph_batch_set_timing")
+
+    def read_timing(self):
+        """(solves, active-set kernel ms total, PDHG kernel ms total); syncs."""
+        out = np.zeros(3)
+        _native.check(self.lib.ph_batch_read_timing(self.handle, out.ctypes.data_as(_native._c_ptr)),
+                      "ph_batch_read_timing")
+        return int(out[0]), float(out[1]), float(out[2])
+
+    def kernel_ms_all(self):
+        """Durations (ms) of every solve recorded in event_log (synchronises)."""
+        if self.event_log:
+            self.event_log[-1][1].synchronize()
+        return [e0.elapsed_time(e1) for e0, e1 in self.event_log]
+
     def summary(self):
         """(not optimal, sum of PDHG iterations, max iterations, polished) of the
         last solve; synchronises the stream (one 32-byte copy)."""
         _native.check(self.lib.ph_batch_solve_summary(
             self.handle, self._summary.ctypes.data_as(_native._c_ptr)), "ph_batch_solve_summary")
         return tuple(int(v) for v in self._summary)
+
+    def set_stream(self, stream_handle):
+        """Point the library's launches at another HIP stream (a raw handle)."""
+        _native.check(self.lib.ph_batch_set_stream(self.handle, ctypes.c_void_p(stream_handle)),
+                      "ph_batch_set_stream")
+
+    @property
+    def stream_handle(self):
+        return self._stream_handle
+
+    # ---- device-side iteration control (ph_loop_* in include/phgpu.h)
+    def loop_reset(self, start_iter, iter_limit, convthresh):
+        _native.check(self.lib.ph_loop_reset(self.handle, int(start_iter), int(iter_limit),
+                                             float(convthresh)), "ph_loop_reset")
+
+    def loop_enable(self, on):
+        _native.check(self.lib.ph_loop_enable(self.handle, 1 if on else 0), "ph_loop_enable")
+
+    def loop_set_xbar(self, prob_coeff, slot_k, slot_s0, slot_s1, out):
+        """Let the post-solve kernel compute the next iteration's xbar sums."""
+        G = 0 if slot_k is None else slot_k.numel()
+        _native.check(self.lib.ph_loop_set_xbar(self.handle, _native.ptr(self.x),
+                                                _native.ptr(prob_coeff), G, _native.ptr(slot_k),
+                                                _native.ptr(slot_s0), _native.ptr(slot_s1),
+                                                _native.ptr(out)), "ph_loop_set_xbar")
+
+    def loop_conv_local(self, absdiff, seg, cnt, nproc, parts, conv_hist):
+        _native.check(self.lib.ph_loop_conv_local(self.handle, _native.ptr(absdiff), _native.ptr(seg),
+                                                  seg.numel() - 1, _native.ptr(cnt), float(nproc),
+                                                  _native.ptr(parts), _native.ptr(conv_hist)),
+                      "ph_loop_conv_local")
+
+    def loop_conv(self, parts, cnt, nproc, conv_hist):
+        _native.check(self.lib.ph_loop_conv(self.handle, _native.ptr(parts), _native.ptr(cnt),
+                                            parts.numel(), float(nproc),
+                                            _native.ptr(conv_hist)), "ph_loop_conv")
+
+    def loop_status(self):
+        """(stop, iter, not-optimal solves, solves, PDHG iters sum, max, polished);
+        synchronises.  stop: 0 running, 1 converged, 2 iteration limit."""
+        out = np.zeros(7, dtype=np.int64)
+        _native.check(self.lib.ph_loop_status(self.handle, out.ctypes.data_as(_native._c_ptr)),
+                      "ph_loop_status")
+        return tuple(int(v) for v in out)
 
     def xbar_accum(self, prob_coeff, slot_k, slot_s0, slot_s1, out):
         G = slot_k.numel()

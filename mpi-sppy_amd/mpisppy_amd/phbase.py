@@ -109,6 +109,9 @@ class PHBase(SPBase):
         self.conv_seg = torch.tensor(seg, **i32)
         self.conv_cnt = np.array([max(len(sl), 1) * K for sl in slices], dtype=np.float64)
         self.conv_parts = torch.zeros(R, **f64)
+        self.conv_cnt_dev = torch.as_tensor(self.conv_cnt, **f64)
+        self.conv_hist = None
+        self._loop_graphs = {}
         self.scenario_feasible = np.ones(S, dtype=bool)
         self._all_feasible = True
 
@@ -425,8 +428,128 @@ class PHBase(SPBase):
         self.current_solver_options = self.PHoptions["iterk_solver_options"]
         return self.trivial_bound
 
+    # ------------------------------------------------- device-side loop --
+    def _device_loop_ok(self):
+        """The iterk_loop body can run without a host round trip per iteration
+        when nothing on the host has to see each iteration (no extensions,
+        converger, hub/spoke communicator or per-iteration printing)."""
+        o = self.PHoptions
+        return (o.get("device_loop", True) and self.PH_extensions is None
+                and self.PH_converger is None and self.spcomm is None
+                and not o["display_progress"] and not o["display_convergence_detail"]
+                and not o.get("display_timing", False))
+
+    def _device_iteration(self, kw):
+        """One iterk_loop pass queued on the device (phbase.py:1498-1553 order):
+        Compute_Xbar -> Update_W -> convergence_diff -> [stop?] -> solve.
+        Compute_Xbar's local sums of this pass were computed by the previous
+        pass's post-solve kernel (or before the first pass); Compute_Xbar's
+        broadcast and Update_W are one kernel (update_w with W), which writes
+        what the two reference calls write."""
+        b = self.batch
+        self.comm.allreduce_(self.xsums)
+        b.update_w(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
+                   self.xsqbar, self.W, self.absdiff)
+        if self.comm.size == 1:
+            b.loop_conv_local(self.absdiff, self.conv_seg, self.conv_cnt_dev, self.ref_n_proc,
+                              self.conv_parts, self.conv_hist)
+        else:
+            b.segment_sum(self.absdiff, None, self.conv_seg, self.conv_parts)
+            self.comm.allreduce_(self.conv_parts)
+            b.loop_conv(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc, self.conv_hist)
+        b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
+
+    def run_device_loop(self, start_iter, iter_limit, convthresh, chunk=None):
+        """Run iterk_loop passes start_iter+1 .. iter_limit on the device,
+        queued `chunk` at a time; the stop flag (convergence or the limit) is
+        read once per chunk.  Returns (stop, last iteration)."""
+        if self.batch is None:
+            self._create_solvers()
+        kw = self._solve_kwargs(self.current_solver_options)
+        b = self.batch
+        chunk = int(chunk or self.PHoptions.get("device_loop_chunk", 16))
+        if self.conv_hist is None or self.conv_hist.numel() < max(iter_limit, 1):
+            self.conv_hist = torch.zeros(max(iter_limit, 1024), dtype=torch.float64,
+                                         device=self.device)
+            self._loop_graphs = {}  # captured pointers changed
+        b.loop_reset(start_iter, iter_limit, convthresh)
+        b.loop_enable(True)
+        b.loop_set_xbar(self.prob_coeff, self.slot_k, self.slot_s0, self.slot_s1, self.xsums)
+        # Compute_Xbar's local sums for the first pass
+        b.xbar_accum(self.prob_coeff, self.slot_k, self.slot_s0, self.slot_s1, self.xsums)
+        graph = None
+        if self._graph_ok():
+            key = (self.w_on, self.prox_on, tuple(sorted(kw.items())), chunk)
+            graph = self._loop_graphs.get(key)
+            if graph is None:
+                graph = self._capture_chunk(kw, chunk)
+                self._loop_graphs[key] = graph
+        try:
+            while True:
+                t0 = time.perf_counter()
+                if graph is not None:
+                    graph.replay()
+                else:
+                    for _ in range(chunk):
+                        self._device_iteration(kw)
+                st = b.loop_status()
+                dt = time.perf_counter() - t0
+                stop, it, nonopt, nsolves, it_sum, it_max, npol = st
+                prev = getattr(self, "_loop_prev", (0, 0))
+                self._loop_prev = (nsolves, npol)
+                if nsolves > prev[0]:
+                    self.solve_log.append((nsolves - prev[0], dt, it_sum / max(nsolves, 1),
+                                           it_max, npol - prev[1]))
+                if stop:
+                    break
+        finally:
+            b.loop_enable(False)
+            b.loop_set_xbar(None, None, None, None, None)
+            self._loop_prev = (0, 0)
+        if nonopt:
+            status = b.status.cpu().numpy()
+            self.scenario_feasible = (status == 0) | (status == 1)
+            if not np.all(self.scenario_feasible):
+                for i in np.nonzero(~self.scenario_feasible)[0]:
+                    print(f"[{type(self).__name__}] Solve failed for scenario "
+                          f"{self.local_scenario_names[i]}")
+        return stop, it
+
+    def _graph_ok(self):
+        """Replay chunks of the device loop as one HIP graph: a single GPU rank
+        (collectives stay eager) on a CUDA device."""
+        return (self.PHoptions.get("device_loop_graphs", True) and self.comm.size == 1
+                and self.device.type == "cuda" and hasattr(self.batch, "set_stream"))
+
+    def _capture_chunk(self, kw, chunk):
+        """Capture `chunk` device iterations (the library's launches moved to
+        the capture stream) into a torch.cuda.CUDAGraph."""
+        b = self.batch
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g):
+            b.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+            try:
+                for _ in range(chunk):
+                    self._device_iteration(kw)
+            finally:
+                b.set_stream(b.stream_handle)
+        return g
+
     def iterk_loop(self):
         """phbase.py:1472-1566: Xbar -> W -> conv -> [hub] -> break? -> solve."""
+        if self._device_loop_ok():
+            max_iterations = int(self.PHoptions["PHIterLimit"])
+            stop, it = self.run_device_loop(0, max_iterations, float(self.PHoptions["convthresh"]))
+            self._PHIter = it
+            hist = self.conv_hist[:it].cpu().numpy() if it > 0 else np.zeros(0)
+            self.conv_history = [float(v) for v in hist]
+            self.conv = self.conv_history[-1] if it > 0 else None
+            if stop == 1:
+                global_toc("Convergence metric=%f dropped below user-supplied threshold=%f"
+                           % (self.conv, self.PHoptions["convthresh"]),
+                           self.cylinder_rank == 0 and self.PHoptions["verbose"])
+            return
         verbose = self.PHoptions["verbose"]
         have_extensions = self.PH_extensions is not None
         have_converger = self.PH_converger is not None

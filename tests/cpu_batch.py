@@ -31,7 +31,70 @@ class CPUBatch:
         d = self.data
         return sp.csr_matrix((d.vals[:, s], d.col_idx, d.row_ptr), shape=(d.m, d.n))
 
+    # ---- device-loop emulation (ph_loop_* semantics of include/phgpu.h)
+    _loop = False
+    _ctl = None
+
+    _xa = None
+
+    def loop_reset(self, start_iter, iter_limit, convthresh):
+        self._ctl = dict(stop=0, iter=int(start_iter), limit=int(iter_limit),
+                         thresh=float(convthresh), acc=[0, 0, 0, 0, 0])
+        self._advance()
+
+    def _advance(self):
+        c = self._ctl
+        if c["stop"]:
+            return
+        if c["iter"] >= c["limit"]:
+            c["stop"] = 2
+        else:
+            c["iter"] += 1
+
+    def loop_enable(self, on):
+        self._loop = bool(on)
+
+    def _stopped(self):
+        return self._loop and self._ctl["stop"] != 0
+
+    def loop_set_xbar(self, prob_coeff, slot_k, slot_s0, slot_s1, out):
+        self._xa = None if slot_k is None else (prob_coeff, slot_k, slot_s0, slot_s1, out)
+
+    def loop_conv_local(self, absdiff, seg, cnt, nproc, parts, conv_hist):
+        if self._stopped():
+            return
+        self.segment_sum(absdiff, None, seg, parts)
+        self.loop_conv(parts, cnt, nproc, conv_hist)
+
+    def loop_conv(self, parts, cnt, nproc, conv_hist):
+        c = self._ctl
+        if c["stop"]:
+            return
+        v = 0.0
+        for r in range(parts.numel()):
+            v += float(parts[r]) / float(cnt[r])
+        v /= nproc
+        conv_hist[c["iter"] - 1] = v
+        if v < c["thresh"]:
+            c["stop"] = 1
+
+    def loop_status(self):
+        c = self._ctl
+        return (c["stop"], c["iter"], *c["acc"])
+
     def solve(self, W, rho, xbar, w_on, prox_on, **kw):
+        if self._stopped():
+            return
+        self._solve(W, rho, xbar, w_on, prox_on)
+        if self._loop:
+            a = self._ctl["acc"]
+            a[0] += int(np.sum(self.status.numpy() != 0))
+            a[1] += self.S
+            if self._xa is not None:
+                self.xbar_accum(*self._xa)
+            self._advance()
+
+    def _solve(self, W, rho, xbar, w_on, prox_on):
         d = self.data
         Wv = W.view(self.K, self.S).numpy(); rv = rho.view(self.K, self.S).numpy()
         xb = xbar.view(self.K, self.S).numpy()
@@ -54,6 +117,8 @@ class CPUBatch:
         return int(np.sum(st != 0)), int(it.sum()), int(it.max(initial=0)), 0
 
     def xbar_accum(self, prob_coeff, slot_k, slot_s0, slot_s1, out):
+        if self._stopped():
+            return
         X = self.x.view(self.n, self.S)[self.cols]
         pc = prob_coeff.view(self.K, self.S)
         G = slot_k.numel()
@@ -63,6 +128,8 @@ class CPUBatch:
             out[G + g] = (pc[k, a:b] * X[k, a:b] ** 2).sum()
 
     def update_w(self, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff):
+        if self._stopped():
+            return
         X = self.x.view(self.n, self.S)[self.cols]
         gi = gid.view(self.K, self.S).long()
         xb = sums[:G][gi]
@@ -77,6 +144,8 @@ class CPUBatch:
         absdiff.copy_(d.abs().sum(0))
 
     def segment_sum(self, v, w, seg, out):
+        if self._stopped():
+            return
         for r in range(seg.numel() - 1):
             a, b = int(seg[r]), int(seg[r + 1])
             out[r] = (v[a:b] * (w[a:b] if w is not None else 1.0)).sum()
