@@ -173,10 +173,11 @@ def run():
     b.set_timing(True)
     ph.run_device_loop(args.warmup + args.steps, args.warmup + 2 * args.steps, -1.0,
                        chunk=args.steps)
-    n_t, as_ms, pd_ms = b.read_timing()
+    n_t, as_ms, po_ms, pd_ms = b.read_timing()
     b.set_timing(False)
     ph.PHoptions["device_loop_graphs"] = True
     as_ms /= max(n_t, 1)
+    po_ms /= max(n_t, 1)
     pd_ms /= max(n_t, 1)
 
     S_loc = ph.S_loc
@@ -265,6 +266,7 @@ def run():
                          "kernel_ms": round(kms, 4),
                          "alg_bytes_per_launch": kbytes,
                          "kernels_ms": {"active_set_kernel": round(as_ms, 4),
+                                        "polish_kernel": round(po_ms, 4),
                                         "pdhg_kernel": round(pd_ms, 4)},
                          "note": "per-launch averages from HIP events on the launch stream over "
                                  "the `steps` PH iterations that follow the timed region (same "

@@ -221,13 +221,13 @@ int ph_loop_status(ph_batch_t b, int64_t *out /*host [7]*/);
 
 /*
  * Kernel timing of ph_pdhg_solve with HIP events recorded on the batch's
- * stream around the active-set kernel and the PDHG kernel of every solve
- * while timing is on (set_timing clears the record).  read_timing
- * synchronises and returns out[3] = {solves recorded, total active-set
- * kernel ms, total PDHG kernel ms}.  (Measurement support; bench.py.)
+ * stream around its kernels of every solve while timing is on (set_timing
+ * clears the record).  read_timing synchronises and returns out[4] =
+ * {solves recorded, total ms of the active-set kernel, of the polish
+ * kernel, of the PDHG kernel}.  (Measurement support; bench.py.)
  */
 int ph_batch_set_timing(ph_batch_t b, int32_t on);
-int ph_batch_read_timing(ph_batch_t b, double *out /*host [3]*/);
+int ph_batch_read_timing(ph_batch_t b, double *out /*host [4]*/);
 
 /* Block until all work queued on the batch's stream has finished. */
 int ph_batch_sync(ph_batch_t b);

@@ -300,7 +300,10 @@ struct SolveArgs {
   // scenarios for pdhg_kernel: wl == null -> all S, else wl[0 .. *wl_count)
   int32_t *wl, *wl_count;
   int32_t *queue;  // work-queue counter (0 at launch)
+  // misses polish_kernel could not finish (pdhg_kernel's list when set)
+  int32_t *wl2, *wl2_count;
   const LoopCtl *ctl;  // device loop control or null
+  unsigned long long *prof;  // [16] phase clocks of the warm polish, or null
 };
 
 // Active-set polish: largest KKT system (free columns + active rows) and the
@@ -818,8 +821,13 @@ __device__ __forceinline__ PolishRes polish_wave(const SolveArgs &a, int s, Poli
     as.signature(sig);
     if (same_sig(sig, prev)) break;  // cycle
     for (int i = 0; i < 4; ++i) prev[i] = sig[i];
+    const unsigned long long tp0 = a.prof ? wall_clock64() : 0ull;
     const AsSol r = active_set_solve(lane, n, m, as, d.G, d.Q, d.L, d.U, d.RL, d.RU, d.DC, d.kslot,
                                      Ka, a.P.row_ptr, a.P.col_idx, vs, kkt, cpos, xs);
+    if (a.prof && lane == 0) {
+      atomicAdd(&a.prof[3], 1ull);
+      atomicAdd(&a.prof[4], wall_clock64() - tp0);
+    }
     const double XU = r.xu, YU = r.yu;
     const double xn = lane < n ? clampd(XU, d.L, d.U) : 0.0;
     const double yn = lane < m ? YU : 0.0;
@@ -837,8 +845,10 @@ __device__ __forceinline__ PolishRes polish_wave(const SolveArgs &a, int s, Poli
     double ep, ed, eg, pobj, dobj;
     kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
     if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
+      const unsigned long long tp1 = a.prof ? wall_clock64() : 0ull;
       if (a.cache)
         cache_store(lane, n, m, a, s, r, kkt, XU, YU, d.HL, d.Q, xs, ys, rowdot, coldot);
+      if (a.prof && lane == 0) atomicAdd(&a.prof[5], wall_clock64() - tp1);
       res.ok = 1;
       res.XN = xn;
       res.YN = yn;
@@ -871,6 +881,7 @@ __device__ __forceinline__ PolishRes polish_wave(const SolveArgs &a, int s, Poli
 // ------------------------------------------------------------------------
 template <int BLOCK, int P, int E>
 __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, double *lds) {
+  const unsigned long long t_start = a.prof ? wall_clock64() : 0ull;
   constexpr int CPT = P, RPT = P;
   constexpr bool POL = (BLOCK == WAVE && P == 1);  // polish needs lane == line
   const int T = blockDim.x;
@@ -1094,13 +1105,20 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
       }
       // start from the active-set kernel's primal-dual active-set step when
       // the cached map missed, else from the warm point's active set
+      const unsigned long long tw0 = a.prof ? wall_clock64() : 0ull;
       unsigned long long hs[4];
       const bool hv = a.hint_ok && a.hint_ok[s];
       if (hv)
         for (int i = 0; i < 4; ++i) hs[i] = a.hint[4 * (size_t)s + i];
       bool ok = false;
-      for (int attempt = hv ? 0 : 1; attempt < 2 && !ok; ++attempt)
-        ok = polish_run(1e-9, POLISH_ROUNDS, attempt == 0 ? hs : nullptr);
+      int att = hv ? 0 : 1;
+      for (; att < 2 && !ok; ++att) ok = polish_run(1e-9, POLISH_ROUNDS, att == 0 ? hs : nullptr);
+      if (a.prof && tid == 0) {
+        atomicAdd(&a.prof[0], 1ull);
+        atomicAdd(&a.prof[1], tw0 - t_start);
+        atomicAdd(&a.prof[2], wall_clock64() - tw0);
+        atomicAdd(&a.prof[ok ? (att == 1 ? 6 : 7) : 8], 1ull);
+      }
       if (ok) {
         stat = PH_STATUS_OPTIMAL;
         how = 1;
@@ -1331,28 +1349,59 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Copy `len` contiguous doubles to LDS with one wave: all loads of a batch of
+// four per lane issued before any store (one memory round trip per 256).
+__device__ __forceinline__ void wave_stage(double *dst, const double *__restrict__ src, int len,
+                                           int lane) {
+  for (int q0 = 0; q0 < len; q0 += 4 * WAVE) {
+    double t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = q0 + u * WAVE + lane;
+      t[u] = q < len ? src[q] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = q0 + u * WAVE + lane;
+      if (q < len) dst[q] = t[u];
+    }
+  }
+}
+
 template <int WPB>
 __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
-  __shared__ double sh[WPB][WAVE];
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x / WAVE;
   const int s = blockIdx.x * WPB + w;
   if (s >= a.S || stopped(a.ctl)) return;  // wave-uniform; no block barriers
   const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m);
-  // ---- every load of the scenario is independent of the others: one
-  // round trip to memory (the entry's validity is checked afterwards)
+  const int SBW = 4 * n + 3 * m;
+  // ---- the scenario's cache entry and static block, staged through LDS by
+  // coalesced loads (one round trip), plus the PH terms and the flag
+  double *ent = lds + (size_t)w * (a.CW + SBW + WAVE);
+  double *sb = ent + a.CW;
+  double *xsw = sb + SBW;  // [WAVE] scratch for the clipped case
   const int ok = a.cache_ok[s];
-  const double *cs = a.cache + (size_t)s * a.CW;
-  const double *B = cs + K;
-  const double *sb = a.sb + (size_t)s * (4 * n + 3 * m);
+  double hk_l = 0.0, qk_l = 0.0, cst_l = 0.0;
+  if (lane < K) {
+    const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
+    const double xb = a.xbar[(size_t)lane * S + s];
+    hk_l = a.w_on * W - a.prox_on * r * xb;
+    qk_l = a.prox_on * r;
+    cst_l = a.prox_on * 0.5 * r * xb * xb;
+  }
+  const int kslot = lane < n ? a.slot_of_col[lane] : -1;
+  wave_stage(ent, a.cache + (size_t)s * a.CW, a.CW, lane);
+  wave_stage(sb, a.sb + (size_t)s * SBW, SBW, lane);
+  wsync();
+  const double *B = ent + K;
   double DC = 1.0, G = 0.0, L = 0.0, U = 0.0, XU = 0.0, ATY = 0.0;
-  int kslot = -1;
   if (lane < n) {
     G = sb[lane];
     L = sb[n + lane];
     U = sb[2 * n + lane];
     DC = sb[3 * n + lane];
-    kslot = a.slot_of_col[lane];
     XU = B[cv_x(n, m) + lane];
     ATY = B[cv_aty(n, m) + lane];
   }
@@ -1364,36 +1413,18 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
     YU = B[cv_y(n, m) + lane];
     AX = B[cv_ax(n, m) + lane];
   }
-  // slot k's PH data at lane k
-  double hk_l = 0.0, qk_l = 0.0, cst_l = 0.0, key_l = 0.0;
-  if (lane < K) {
-    const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
-    const double xb = a.xbar[(size_t)lane * S + s];
-    hk_l = a.w_on * W - a.prox_on * r * xb;
-    qk_l = a.prox_on * r;
-    cst_l = a.prox_on * 0.5 * r * xb * xb;
-    key_l = cs[lane];
-  }
-  // v(h) = base + sum_k h_k D_k, KB slots per batch of independent loads
-  constexpr int KB = 1;
-  for (int k0 = 0; k0 < K; k0 += KB) {
-    double dx[KB], dy[KB], dax[KB], daty[KB];
-#pragma unroll
-    for (int t = 0; t < KB; ++t) {
-      const double *Dk = B + (size_t)(k0 + t + 1) * VL;
-      const bool on = k0 + t < K;
-      dx[t] = (on && lane < n) ? Dk[cv_x(n, m) + lane] : 0.0;
-      daty[t] = (on && lane < n) ? Dk[cv_aty(n, m) + lane] : 0.0;
-      dy[t] = (on && lane < m) ? Dk[cv_y(n, m) + lane] : 0.0;
-      dax[t] = (on && lane < m) ? Dk[cv_ax(n, m) + lane] : 0.0;
+  const double key_l = lane < K ? ent[lane] : 0.0;
+  // v(h) = base + sum_k h_k D_k (from LDS)
+  for (int k = 0; k < K; ++k) {
+    const double hk = __shfl(hk_l, k & (WAVE - 1), WAVE);
+    const double *Dk = B + (size_t)(k + 1) * VL;
+    if (lane < n) {
+      XU = fma(hk, Dk[cv_x(n, m) + lane], XU);
+      ATY = fma(hk, Dk[cv_aty(n, m) + lane], ATY);
     }
-#pragma unroll
-    for (int t = 0; t < KB; ++t) {
-      const double hk = __shfl(hk_l, (k0 + t) & (WAVE - 1), WAVE);
-      XU = fma(hk, dx[t], XU);
-      ATY = fma(hk, daty[t], ATY);
-      YU = fma(hk, dy[t], YU);
-      AX = fma(hk, dax[t], AX);
+    if (lane < m) {
+      YU = fma(hk, Dk[cv_y(n, m) + lane], YU);
+      AX = fma(hk, Dk[cv_ax(n, m) + lane], AX);
     }
   }
   // the slot's h and q moved to its column
@@ -1416,10 +1447,9 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   double ATYN = ATY;
   if (__ballot(lane < n && XN != XU)) {
     // a column left its bounds: the products of the clipped point by SpMV
-    double *xs = sh[w];
-    if (lane < n) xs[lane] = XN;
+    if (lane < n) xsw[lane] = XN;
     wsync();
-    AXN = pat_rowdot(lane, m, a.P, a.vals_s + (size_t)s * a.nnz, xs);
+    AXN = pat_rowdot(lane, m, a.P, a.vals_s + (size_t)s * a.nnz, xsw);
   }
   double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   double lam = 0.0;
@@ -1481,6 +1511,7 @@ __global__ void loop_conv_kernel(LoopCtl *c, const double *__restrict__ parts,
   if (v < c->thresh) c->stop = 1;
   ctr[0] = 0;
   ctr[1] = 0;
+  ctr[2] = 0;
 }
 
 // Single-rank form: the per-reference-rank sums of absdiff over the
@@ -1494,7 +1525,13 @@ __global__ void __launch_bounds__(1024) loop_conv_local_kernel(
   double conv = 0.0;
   for (int r = 0; r < R; ++r) {
     double acc[1] = {0.0};
-    for (int s = seg[r] + threadIdx.x; s < seg[r + 1]; s += blockDim.x) acc[0] += v[s];
+    const int e = seg[r + 1], bd = blockDim.x;
+    for (int s0 = seg[r] + threadIdx.x; s0 < e; s0 += 4 * bd) {
+      double t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = s0 + u * bd < e ? v[s0 + u * bd] : 0.0;
+      acc[0] += (t[0] + t[1]) + (t[2] + t[3]);
+    }
     block_sum<1>(acc, red);
     if (threadIdx.x == 0) parts[r] = acc[0];
     conv += acc[0] / cnt[r];
@@ -1505,6 +1542,345 @@ __global__ void __launch_bounds__(1024) loop_conv_local_kernel(
     if (conv < c->thresh) c->stop = 1;
     ctr[0] = 0;
     ctr[1] = 0;
+    ctr[2] = 0;
+  }
+}
+
+// ------------------------------------------------------------------------
+// polish_kernel: the misses of the active-set cache (work list wl), one
+// wave per scenario (lane t owns column t and row t).  Starting from the
+// active-set kernel's primal-dual active-set step (the hint), each round
+// solves the active set's KKT system by Gauss-Jordan elimination with the
+// matrix held in registers -- lane r owns equation row r, RG_W columns:
+// the N unknowns (x of the free columns, then y of the active rows), and
+// from column RG_R0 on the right-hand sides (the current objective, then
+// d/dh_k of the K PH terms) -- so one pivot step is a DPP max-reduction
+// for the pivot, a readlane broadcast of the pivot row and one FMA per
+// remaining column: no LDS round trip per row.  Accepted (KKT check at
+// a.tol) -> written out and the cache entry refreshed; otherwise PDAS
+// re-classification, and after POLISH_ROUNDS the scenario goes to
+// pdhg_kernel (wl2).  Scenarios outside the register shape (N > RG_R0 or
+// K > RG_K) go to pdhg_kernel directly.
+// ------------------------------------------------------------------------
+constexpr int RG_W = 32;               // register row width
+constexpr int RG_K = 8;                // parametric right-hand sides
+constexpr int RG_R0 = RG_W - 1 - RG_K; // first right-hand-side column = max unknowns
+
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v & 0xffffffffull), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xF, 0xF, false);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v & 0xffffffffull), l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __longlong_as_double((long long)readlane_u64((unsigned long long)__double_as_longlong(v), l));
+}
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) {
+  return a > b ? a : b;
+}
+// wave-wide max of a 64-bit key, uniform result: DPP within rows of 16
+// lanes (xor 1, xor 2, half-mirror, mirror), then the four row maxima
+__device__ __forceinline__ unsigned long long wave_max_key(unsigned long long v) {
+  v = umax64(v, dpp_u64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = umax64(v, dpp_u64<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = umax64(v, dpp_u64<0x141>(v));  // row_half_mirror
+  v = umax64(v, dpp_u64<0x140>(v));  // row_mirror
+  return umax64(umax64(readlane_u64(v, 0), readlane_u64(v, 16)),
+                umax64(readlane_u64(v, 32), readlane_u64(v, 48)));
+}
+__device__ __forceinline__ unsigned long long abs_key(double v) {  // order of |v| as u64
+  return (unsigned long long)__double_as_longlong(fabs(v));
+}
+
+__global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x;
+  const int S = a.S, n = a.n, m = a.m, nnz = a.nnz, K = a.K;
+  const int count = stopped(a.ctl) ? 0 : *a.wl_count;
+  if ((int)blockIdx.x >= count) return;
+  // LDS: staging rows | solutions | vals | xs | ys | pattern + maps
+  double *kst = lds;                        // [RG_R0][RG_W]
+  double *sol = kst + RG_R0 * RG_W;         // [1+RG_K][WAVE]
+  double *vl = sol + (1 + RG_K) * WAVE;     // [nnz]
+  double *xs = vl + nnz;                    // [WAVE]
+  double *ys = xs + WAVE;                   // [WAVE]
+  int32_t *rp = (int32_t *)(ys + WAVE);     // [m+1]
+  int32_t *ci = rp + (m + 1);               // [nnz]
+  int32_t *cp = ci + nnz;                   // [n+1]
+  int32_t *cr = cp + (n + 1);               // [nnz]
+  int32_t *ck = cr + nnz;                   // [nnz]
+  int32_t *cpos = ck + nnz;                 // [WAVE]
+  int32_t *rpos = cpos + WAVE;              // [WAVE]
+  for (int q = lane; q <= m; q += WAVE) rp[q] = a.P.row_ptr[q];
+  for (int q = lane; q <= n; q += WAVE) cp[q] = a.P.col_ptr[q];
+  for (int q = lane; q < nnz; q += WAVE) {
+    ci[q] = a.P.col_idx[q];
+    cr[q] = a.P.csc_row[q];
+    ck[q] = a.P.csc_k[q];
+  }
+  const int kslot = lane < n ? a.slot_of_col[lane] : -1;
+  auto rowdot = [&]() {  // row `lane` of A xs
+    double acc = 0.0;
+    if (lane < m)
+      for (int p = rp[lane]; p < rp[lane + 1]; ++p) acc = fma(vl[p], xs[ci[p]], acc);
+    return acc;
+  };
+  auto coldot = [&]() {  // column `lane` of A' ys
+    double acc = 0.0;
+    if (lane < n)
+      for (int p = cp[lane]; p < cp[lane + 1]; ++p) acc = fma(vl[ck[p]], ys[cr[p]], acc);
+    return acc;
+  };
+  unsigned long long tq = a.prof ? wall_clock64() : 0ull;  // phase clock (debug)
+  auto tick = [&](int slot) {
+    if (a.prof) {
+      const unsigned long long t = wall_clock64();
+      if (lane == 0) atomicAdd(&a.prof[slot], t - tq);
+      tq = t;
+    }
+  };
+  for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
+    const int s = a.wl[idx];
+    __syncthreads();  // LDS of the previous scenario
+    tick(9);  // pattern copy / previous scenario's tail
+    // ---- scenario data (scaled): static block, PH terms, values
+    const double *sb = a.sb + (size_t)s * (4 * n + 3 * m);
+    double G = 0.0, L = 0.0, U = 0.0, DC = 1.0, RL = 0.0, RU = 0.0, DR = 1.0;
+    if (lane < n) {
+      G = sb[lane];
+      L = sb[n + lane];
+      U = sb[2 * n + lane];
+      DC = sb[3 * n + lane];
+    }
+    if (lane < m) {
+      RL = sb[4 * n + lane];
+      RU = sb[4 * n + m + lane];
+      DR = sb[4 * n + 2 * m + lane];
+    }
+    double hk_l = 0.0, qk_l = 0.0, cst_l = 0.0;
+    if (lane < K) {
+      const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
+      const double xb = a.xbar[(size_t)lane * S + s];
+      hk_l = a.w_on * W - a.prox_on * r * xb;
+      qk_l = a.prox_on * r;
+      cst_l = a.prox_on * 0.5 * r * xb * xb;
+    }
+    unsigned long long sig0[4];
+    for (int i = 0; i < 4; ++i) sig0[i] = a.hint[4 * (size_t)s + i];
+    const double *vs = a.vals_s + (size_t)s * nnz;
+    for (int q = lane; q < nnz; q += WAVE) vl[q] = vs[q];
+    const double HL = __shfl(hk_l, kslot >= 0 ? kslot : 0, WAVE) * (kslot >= 0 ? 1.0 : 0.0);
+    const double qj = __shfl(qk_l, kslot >= 0 ? kslot : 0, WAVE);
+    G += HL * DC;
+    const double Q = (kslot >= 0 ? qj : 0.0) * DC * DC;
+    const double cst = wave_sum(cst_l);
+    ActiveSet as = set_from_sig(lane, sig0);
+    unsigned long long prev[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    bool done = K > RG_K;
+    tick(10);  // scenario loads  // outside the register shape: straight to pdhg_kernel
+    bool solved = false;
+    for (int round = 0; round < POLISH_ROUNDS && !done; ++round) {
+      unsigned long long sig[4];
+      as.signature(sig);
+      if (same_sig(sig, prev)) break;  // cycle
+      for (int i = 0; i < 4; ++i) prev[i] = sig[i];
+      // ---- the active set's KKT system
+      const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      const bool fr = lane < n && as.cs == 0;
+      const bool ac = lane < m && as.rs != 0;
+      const unsigned long long fm = __ballot(fr), am = __ballot(ac);
+      const int nF = __popcll(fm), N = nF + __popcll(am);
+      if (N > RG_R0) break;
+      const int pF = __popcll(fm & below), pR = nF + __popcll(am & below);
+      const double xfix = as.cs == 1 ? L : (as.cs == 2 ? U : 0.0);
+      __syncthreads();
+      if (lane < n) {
+        cpos[lane] = fr ? pF : -1;
+        xs[lane] = xfix;
+      }
+      if (lane < m) rpos[lane] = ac ? pR : -1;
+      for (int q = lane; q < RG_R0 * RG_W; q += WAVE) kst[q] = 0.0;
+      for (int q = lane; q < (1 + RG_K) * WAVE; q += WAVE) sol[q] = 0.0;
+      __syncthreads();
+      if (fr) {  // stationarity row of free column `lane`
+        double *row = kst + pF * RG_W;
+        row[pF] = Q;
+        row[RG_R0] = -G;
+        if (kslot >= 0) row[RG_R0 + 1 + kslot] = -DC;
+        for (int p = cp[lane]; p < cp[lane + 1]; ++p) {
+          const int e = rpos[cr[p]];
+          if (e >= 0) row[e] = -vl[ck[p]];
+        }
+      }
+      if (ac) {  // active row `lane`
+        double *row = kst + pR * RG_W;
+        double rhs = as.rs == 1 ? RL : RU;
+        for (int p = rp[lane]; p < rp[lane + 1]; ++p) {
+          const int j = ci[p];
+          const int e = cpos[j];
+          if (e >= 0) row[e] = vl[p];
+          else rhs -= vl[p] * xs[j];
+        }
+        row[RG_R0] = rhs;
+      }
+      __syncthreads();
+      double rg[RG_W];
+#pragma unroll
+      for (int c = 0; c < RG_W; ++c) rg[c] = lane < N ? kst[lane * RG_W + c] : 0.0;
+      tick(11);  // system build
+      // ---- Gauss-Jordan in registers
+      unsigned long long amax_k = 0ull;
+#pragma unroll
+      for (int c = 0; c < RG_R0; ++c) amax_k = umax64(amax_k, c < N ? abs_key(rg[c]) : 0ull);
+      const double amax = __longlong_as_double((long long)wave_max_key(amax_k));
+      const double piv_min = 1e-11 * (amax > 0.0 ? amax : 1.0);
+      bool used = false;
+      int myunk = -1;
+      double pivv = 1.0;
+#pragma unroll
+      for (int kk = 0; kk < RG_R0; ++kk) {
+        if (kk < N) {
+          const unsigned long long key =
+              (!used && lane < N) ? ((abs_key(rg[kk]) & ~63ull) | (unsigned long long)(63 - lane)) : 0ull;
+          const unsigned long long kmax = wave_max_key(key);
+          const double pabs = __longlong_as_double((long long)(kmax & ~63ull));
+          if (pabs > piv_min) {  // else: dependent column, its unknown stays 0
+            const int p = 63 - (int)(kmax & 63ull);
+            const double piv = readlane_f64(rg[kk], p);
+            const double inv = 1.0 / piv;
+            double prow[RG_W];
+#pragma unroll
+            for (int c = kk + 1; c < RG_W; ++c) prow[c] = readlane_f64(rg[c], p);
+            if (lane == p) {
+              used = true;
+              myunk = kk;
+              pivv = piv;
+            } else {
+              const double f = rg[kk] * inv;
+#pragma unroll
+              for (int c = kk + 1; c < RG_W; ++c) rg[c] = fma(-f, prow[c], rg[c]);
+              rg[kk] = 0.0;
+            }
+          }
+        }
+      }
+      tick(12);  // elimination
+      // unknowns to LDS: sol[t][unknown] for the current rhs (t = 0) and d/dh_k
+      if (used) {
+        const double ip = 1.0 / pivv;
+#pragma unroll
+        for (int t = 0; t <= RG_K; ++t)
+          if (t <= K) sol[t * WAVE + myunk] = rg[RG_R0 + t] * ip;
+      }
+      __syncthreads();
+      const double XU = lane < n ? (fr ? sol[pF] : xfix) : 0.0;
+      const double YU = ac ? sol[pR] : 0.0;
+      // ---- KKT check of the clipped point
+      const double xn = lane < n ? clampd(XU, L, U) : 0.0;
+      const double yn = lane < m ? YU : 0.0;
+      __syncthreads();
+      if (lane < n) xs[lane] = xn;
+      if (lane < m) ys[lane] = yn;
+      __syncthreads();
+      const double axn = rowdot();
+      const double aty = coldot();
+      double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      double lam = 0.0;
+      if (lane < n) kkt_terms_col(xn, G, Q, L, U, DC, aty, lam, v);
+      if (lane < m) kkt_terms_row(axn, yn, RL, RU, DR, v);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) v[i] = wave_sum(v[i]);
+      double ep, ed, eg, pobj, dobj;
+      kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
+      tick(13);  // solution + KKT check
+      if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
+        // ---- accepted: refresh the cache entry (affine map at this h)
+        if (a.cache) {
+          double *cs = a.cache + (size_t)s * a.CW;
+          const int VL = cache_vlen(n, m);
+          __syncthreads();
+          if (lane < n) xs[lane] = XU;
+          if (lane < m) ys[lane] = YU;
+          __syncthreads();
+          double bx = XU, by = YU, bax = rowdot(), baty = coldot();
+          for (int k = 0; k < K; ++k) {
+            const double hk = __shfl(hk_l, k, WAVE);
+            const double dx = fr ? sol[(k + 1) * WAVE + pF] : 0.0;
+            const double dy = ac ? sol[(k + 1) * WAVE + pR] : 0.0;
+            __syncthreads();
+            if (lane < n) xs[lane] = dx;
+            if (lane < m) ys[lane] = dy;
+            __syncthreads();
+            const double dax = rowdot(), daty = coldot();
+            double *Dk = cs + K + (size_t)(k + 1) * VL;
+            if (lane < n) {
+              Dk[cv_x(n, m) + lane] = dx;
+              Dk[cv_aty(n, m) + lane] = daty;
+            }
+            if (lane < m) {
+              Dk[cv_y(n, m) + lane] = dy;
+              Dk[cv_ax(n, m) + lane] = dax;
+            }
+            bx -= hk * dx;
+            by -= hk * dy;
+            bax -= hk * dax;
+            baty -= hk * daty;
+          }
+          double *B = cs + K;
+          const int jk = lane < K ? a.nonant_col[lane] : 0;
+          const double dck = __shfl(DC, jk, WAVE);
+          const double key = qk_l;
+          if (lane < K) cs[lane] = key * dck * dck;  // scaled Q of slot `lane`'s column
+          if (lane < n) {
+            B[cv_x(n, m) + lane] = bx;
+            B[cv_aty(n, m) + lane] = baty;
+          }
+          if (lane < m) {
+            B[cv_y(n, m) + lane] = by;
+            B[cv_ax(n, m) + lane] = bax;
+          }
+          if (lane == 0) a.cache_ok[s] = 1;
+        }
+        tick(14);  // cache store
+        if (a.prof && lane == 0) atomicAdd(&a.prof[15], 1ull);
+        if (lane < n) a.x[(size_t)lane * S + s] = xn * DC;
+        if (lane < m) a.y[(size_t)lane * S + s] = yn * DR;
+        if (lane == 0) {
+          a.status[s] = PH_STATUS_OPTIMAL;
+          a.iters[s] = 0;
+          a.pobj[s] = pobj;
+          a.dbound[s] = dobj;
+          double *dg = a.diag + PH_DIAG_W * (size_t)s;
+          dg[0] = ep;
+          dg[1] = ed;
+          dg[2] = eg;
+          dg[3] = -1.0;
+          dg[4] = 1.0;
+        }
+        solved = true;
+        break;
+      }
+      // ---- primal-dual active-set step from the unclipped solution
+      const bool clipped = __ballot(lane < n && XU != xn) != 0ull;
+      double AXU = axn;
+      const double LAMU = lam + Q * (XU - xn);
+      __syncthreads();
+      if (clipped) {
+        if (lane < n) xs[lane] = XU;
+        __syncthreads();
+        AXU = rowdot();
+      }
+      as = classify_pdas(lane, n, m, XU, LAMU, yn, AXU, L, U, RL, RU);
+    }
+    if (!solved && lane == 0) {  // pdhg_kernel: warm polish from the point, then PDHG
+      a.hint_ok[s] = 0;
+      a.wl2[atomicAdd(a.wl2_count, 1)] = s;
+    }
   }
 }
 
@@ -1524,10 +1900,20 @@ __device__ __forceinline__ void xbar_sums_block(const XbarArgs &xa, int g) {
   const double *xr = xa.x + (size_t)xa.nonant_col[k] * xa.S;
   const double *pr = xa.pc + (size_t)k * xa.S;
   double v[2] = {0.0, 0.0};
-  for (int s = xa.s0[g] + threadIdx.x; s < xa.s1[g]; s += blockDim.x) {
-    const double xv = xr[s], p = pr[s];
-    v[0] += p * xv;
-    v[1] += p * xv * xv;
+  const int s1 = xa.s1[g], bd = blockDim.x;
+  for (int s0 = xa.s0[g] + threadIdx.x; s0 < s1; s0 += 4 * bd) {
+    double xv[4], p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // four independent loads in flight
+      const int s = s0 + u * bd;
+      xv[u] = s < s1 ? xr[s] : 0.0;
+      p[u] = s < s1 ? pr[s] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[0] += p[u] * xv[u];
+      v[1] += p[u] * xv[u] * xv[u];
+    }
   }
   block_sum<2>(v, red);
   if (threadIdx.x == 0) {
@@ -1596,12 +1982,25 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
     return;
   }
   unsigned long long v[4] = {0ull, 0ull, 0ull, 0ull};
-  for (int s = threadIdx.x; s < S; s += blockDim.x) {
-    const unsigned long long it = (unsigned long long)iters[s];
-    v[0] += status[s] != PH_STATUS_OPTIMAL;
-    v[1] += it;
-    v[2] = it > v[2] ? it : v[2];
-    v[3] += diag[PH_DIAG_W * (size_t)s + 4] != 0.0;
+  const int bd = blockDim.x;
+  for (int s0 = threadIdx.x; s0 < S; s0 += 4 * bd) {
+    int st[4], itr[4];
+    double hw[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // independent loads in flight
+      const int s = s0 + u * bd;
+      st[u] = s < S ? status[s] : PH_STATUS_OPTIMAL;
+      itr[u] = s < S ? iters[s] : 0;
+      hw[u] = s < S ? diag[PH_DIAG_W * (size_t)s + 4] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned long long it = (unsigned long long)itr[u];
+      v[0] += st[u] != PH_STATUS_OPTIMAL;
+      v[1] += it;
+      v[2] = it > v[2] ? it : v[2];
+      v[3] += hw[u] != 0.0;
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -1674,14 +2073,15 @@ struct ph_batch {
   double *d_cache = nullptr;
   int32_t *d_cache_ok = nullptr;
   unsigned long long *d_hint = nullptr;
-  int32_t *d_hint_ok = nullptr, *d_wl = nullptr;
-  int32_t *d_ctr = nullptr;  // [2]: work-list count, work-queue counter
+  int32_t *d_hint_ok = nullptr, *d_wl = nullptr, *d_wl2 = nullptr;
+  int32_t *d_ctr = nullptr;  // [4]: miss list count, pdhg queue, pdhg list count
   double *d_sb = nullptr;    // [S][4n+3m] static block (polish-size scenarios)
   LoopCtl *d_ctl = nullptr;  // device loop control
   bool loop_on = false;
   XbarArgs loop_xa{};         // Compute_Xbar sums done by the post-solve kernel (G > 0)
   // optional per-kernel timing of ph_pdhg_solve (HIP events on the stream)
   bool timing = false;
+  unsigned long long *d_prof = nullptr;  // warm-polish phase clocks (ph_debug_prof)
   std::vector<hipEvent_t> ev;  // 4 per recorded solve: as0, as1 (=pd0), pd1, spare
   size_t ev_used = 0;
   int pdhg_grid = 0;         // resident blocks of the pdhg kernel (0: not yet known)
@@ -1815,7 +2215,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
       (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
-      (rc = dalloc(&b->d_summary, 4)) || (rc = dalloc(&b->d_ctr, 2)) || (rc = dalloc(&b->d_ctl, 1)) ||
+      (rc = dalloc(&b->d_summary, 4)) || (rc = dalloc(&b->d_ctr, 4)) || (rc = dalloc(&b->d_ctl, 1)) ||
       (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
@@ -1854,6 +2254,11 @@ int ph_batch_set_stream(ph_batch_t b, void *stream) {
 
 static size_t scale_lds_bytes(const ph_batch *b) {
   return sizeof(double) * ((size_t)b->nnz + 2 * b->m + 2 * b->n + MAX_WAVES * 8);
+}
+constexpr int POLISH_GRID = 2048;  // polish_kernel blocks (one wave each)
+static size_t polish_lds_bytes(const ph_batch *b) {
+  return sizeof(double) * ((size_t)RG_R0 * RG_W + (1 + RG_K) * WAVE + b->nnz + 2 * WAVE) +
+         sizeof(int32_t) * ((size_t)(b->m + 1) + 3 * (size_t)b->nnz + (b->n + 1) + 2 * WAVE);
 }
 static bool polish_fits(const ph_batch *b) {
   return b->block == WAVE && b->per == 1 && b->n + b->m <= POLISH_MAX;
@@ -1921,18 +2326,21 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
   b->K = K;
   // active-set cache for scenarios the one-wave polish covers
   for (void *p : {(void *)b->d_cache, (void *)b->d_cache_ok, (void *)b->d_hint,
-                  (void *)b->d_hint_ok, (void *)b->d_wl})
+                  (void *)b->d_hint_ok, (void *)b->d_wl, (void *)b->d_wl2})
     if (p) (void)hipFree(p);
   b->d_cache = nullptr;
-  b->d_cache_ok = b->d_hint_ok = b->d_wl = nullptr;
+  b->d_cache_ok = b->d_hint_ok = b->d_wl = b->d_wl2 = nullptr;
   b->d_hint = nullptr;
   b->CW = 0;
   b->pdhg_grid = 0;  // LDS per block depends on the cache
-  if (polish_fits(b)) {
-    b->CW = K + (K + 1) * 2 * (b->n + b->m);
+  // active-set cache: for polish-size scenarios whose entry (+ static
+  // block) stages in a quarter of the LDS per 4-wave block
+  const size_t cw = (size_t)K + (K + 1) * 2 * (size_t)(b->n + b->m);
+  if (polish_fits(b) && 4 * 8 * (cw + 4 * b->n + 3 * b->m + WAVE) <= 40 * 1024) {
+    b->CW = (int)cw;
     if ((rc = dalloc(&b->d_cache, (size_t)b->S * b->CW)) || (rc = dalloc(&b->d_cache_ok, b->S)) ||
         (rc = dalloc(&b->d_hint, (size_t)b->S * 4)) || (rc = dalloc(&b->d_hint_ok, b->S)) ||
-        (rc = dalloc(&b->d_wl, b->S)))
+        (rc = dalloc(&b->d_wl, b->S)) || (rc = dalloc(&b->d_wl2, b->S)))
       return rc;
     HIP_OK(hipMemsetAsync(b->d_cache_ok, 0, sizeof(int32_t) * b->S, b->stream));
   }
@@ -1975,7 +2383,10 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.wl = nullptr;
   a.wl_count = b->d_ctr;
   a.queue = b->d_ctr + 1;
+  a.wl2 = nullptr;
+  a.wl2_count = b->d_ctr + 2;
   a.ctl = loop_ctl(b);
+  a.prof = b->d_prof;
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
@@ -1989,18 +2400,18 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     b->pdhg_grid = std::max(1, per_cu) * std::max(1, cus);
   }
   // (in the device loop the convergence kernel has cleared the counters)
-  if (!b->loop_on) HIP_OK(hipMemsetAsync(b->d_ctr, 0, 2 * sizeof(int32_t), b->stream));
+  if (!b->loop_on) HIP_OK(hipMemsetAsync(b->d_ctr, 0, 4 * sizeof(int32_t), b->stream));
   hipEvent_t *tev = nullptr;
   if (b->timing) {
-    if (b->ev_used + 3 > b->ev.size()) {
-      for (int i = 0; i < 3; ++i) {
+    if (b->ev_used + 4 > b->ev.size()) {
+      for (int i = 0; i < 4; ++i) {
         hipEvent_t e;
         HIP_OK(hipEventCreate(&e));
         b->ev.push_back(e);
       }
     }
     tev = &b->ev[b->ev_used];
-    b->ev_used += 3;
+    b->ev_used += 4;
     HIP_OK(hipEventRecord(tev[0], b->stream));
   }
   if (a.cache && a.warm) {
@@ -2008,17 +2419,30 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     a.hint_ok = b->d_hint_ok;
     a.wl = b->d_wl;
     constexpr int WPB = 4;
+    a.wl2 = b->d_wl2;
+    const size_t as_lds = sizeof(double) * WPB * ((size_t)b->CW + 4 * b->n + 3 * b->m + WAVE);
     hipLaunchKernelGGL((active_set_kernel<WPB>), dim3((b->S + WPB - 1) / WPB), dim3(WPB * WAVE),
-                       0, b->stream, a);
+                       as_lds, b->stream, a);
     HIP_OK(hipGetLastError());
+    if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
+    // the misses: register Gauss-Jordan polish; what it cannot finish goes
+    // to pdhg_kernel through the second list
+    hipLaunchKernelGGL(polish_kernel, dim3(std::min(b->S, POLISH_GRID)), dim3(WAVE),
+                       polish_lds_bytes(b), b->stream, a);
+    HIP_OK(hipGetLastError());
+    a.wl = b->d_wl2;
+    a.wl_count = b->d_ctr + 2;
   }
-  if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
+  if (tev) {
+    if (!(a.cache && a.warm)) HIP_OK(hipEventRecord(tev[1], b->stream));
+    HIP_OK(hipEventRecord(tev[2], b->stream));
+  }
   const int grid = std::min(b->S, b->pdhg_grid);
   DISPATCH_GEOM(b->block, b->per, b->ext, {
     hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(grid), dim3(B_), lds, b->stream, a);
   });
   HIP_OK(hipGetLastError());
-  if (tev) HIP_OK(hipEventRecord(tev[2], b->stream));
+  if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
   // device loop: the summary block also advances the iteration, and G
   // more blocks compute the next iteration's Compute_Xbar sums
   const int post_g = (b->loop_on && b->loop_xa.x == x) ? b->loop_xa.G : 0;
@@ -2170,18 +2594,41 @@ int ph_batch_set_timing(ph_batch_t b, int32_t on) {
 int ph_batch_read_timing(ph_batch_t b, double *out) {
   if (!b || !out) return fail(PH_EINVAL, "ph_batch_read_timing: bad arguments");
   HIP_OK(hipStreamSynchronize(b->stream));
-  double t_as = 0.0, t_pd = 0.0;
-  const size_t n = b->ev_used / 3;
-  for (size_t i = 0; i < n; ++i) {
-    float ms0 = 0.f, ms1 = 0.f;
-    HIP_OK(hipEventElapsedTime(&ms0, b->ev[3 * i], b->ev[3 * i + 1]));
-    HIP_OK(hipEventElapsedTime(&ms1, b->ev[3 * i + 1], b->ev[3 * i + 2]));
-    t_as += ms0;
-    t_pd += ms1;
-  }
+  double t[3] = {0.0, 0.0, 0.0};
+  const size_t n = b->ev_used / 4;
+  for (size_t i = 0; i < n; ++i)
+    for (int j = 0; j < 3; ++j) {
+      float ms = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms, b->ev[4 * i + j], b->ev[4 * i + j + 1]));
+      t[j] += ms;
+    }
   out[0] = (double)n;
-  out[1] = t_as;
-  out[2] = t_pd;
+  out[1] = t[0];
+  out[2] = t[1];
+  out[3] = t[2];
+  return PH_OK;
+}
+
+// Debug (not in phgpu.h): phase clocks of pdhg_kernel's warm polish, in
+// 100 MHz ticks.  on != 0 clears and enables, on == 0 disables; read copies
+// out[16] {polishes, prologue, polish, GJ solves, GJ, cache store,
+// ok 1st attempt, ok 2nd attempt, failed}.
+int ph_debug_prof(ph_batch_t b, int32_t on, int64_t *out) {
+  if (!b) return fail(PH_EINVAL, "null batch");
+  if (out && b->d_prof) {
+    HIP_OK(hipMemcpyAsync(out, b->d_prof, 16 * 8, hipMemcpyDeviceToHost, b->stream));
+    HIP_OK(hipStreamSynchronize(b->stream));
+  }
+  if (on) {
+    if (!b->d_prof) {
+      int rc = dalloc(&b->d_prof, 16);
+      if (rc) return rc;
+    }
+    HIP_OK(hipMemsetAsync(b->d_prof, 0, 16 * 8, b->stream));
+  } else if (!out && b->d_prof) {
+    (void)hipFree(b->d_prof);
+    b->d_prof = nullptr;
+  }
   return PH_OK;
 }
 
@@ -2196,7 +2643,8 @@ void ph_batch_destroy(ph_batch_t b) {
   void *ptrs[] = {b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k,
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
-                  b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_ctr, b->d_sb,
+                  b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
+                  b->d_sb,
                   b->d_ctl,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)

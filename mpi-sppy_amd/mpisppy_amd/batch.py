@@ -224,11 +224,11 @@ class DeviceBatch:
                       "ph_batch_set_timing")
 
     def read_timing(self):
-        """(solves, active-set kernel ms total, PDHG kernel ms total); syncs."""
-        out = np.zeros(3)
+        """(solves, total ms of the active-set, polish and PDHG kernels); syncs."""
+        out = np.zeros(4)
         _native.check(self.lib.ph_batch_read_timing(self.handle, out.ctypes.data_as(_native._c_ptr)),
                       "ph_batch_read_timing")
-        return int(out[0]), float(out[1]), float(out[2])
+        return int(out[0]), float(out[1]), float(out[2]), float(out[3])
 
     def kernel_ms_all(self):
         """Durations (ms) of every solve recorded in event_log (synchronises)."""
