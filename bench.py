@@ -3,10 +3,15 @@
 
 A "step" is one PH iteration of the hot path over the whole scenario set:
 Compute_Xbar -> Update_W -> convergence_diff (device kernels + RCCL allreduce)
--> solve_loop (one batched PDHG launch per rank solving every local
-scenario's prox-QP to 1e-9 relative KKT).  Scenarios are split over ranks as
-the reference does (contiguous slices); the total scenario count is fixed, so
-scaling is strong.
+-> solve_loop (the batched solve of every local scenario's prox-QP to 1e-9
+relative KKT).  Steps run through the device-side PH loop (PHBase.
+run_device_loop), replayed as HIP graphs on one GPU.
+
+Scaling is weak: every rank holds --scens scenarios (10,000 by default, the
+BASELINE config on one GPU), so N GPUs solve N x 10,000 scenarios per step;
+scenarios are split over ranks as the reference does (contiguous slices).
+The PH-to-tolerance run ("ph_to_tol") is always the 10,000-scenario instance
+(strong: the same problem on N GPUs).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scens S] [--crops C]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -87,6 +92,26 @@ def cpu_baseline(c, sample_scens, min_seconds=10.0):
                       f"via scipy, sequential on 1 core, {dt:.1f} s"}
 
 
+def pmc_traffic(kname, S_loc, c):
+    """HBM bytes per launch of `kname` from the committed rocprofv3 PMC passes
+    (profiles/r*/pmc_summary.json, written by tools/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE passes of this bench command, gfx950
+    FETCH_SIZE x2 correction applied there), when they were collected on
+    this workload; else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")),
+                       reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kname)
+        if k and d.get("scenarios_per_rank") == S_loc and d.get("crops_multiplier") == c:
+            return k.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     # everything but the final JSON line goes to stderr
     real_stdout = sys.stdout
@@ -104,7 +129,8 @@ def run():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--scens", type=int, default=10000)
+    ap.add_argument("--scens", type=int, default=10000, help="scenarios per rank")
+    ap.add_argument("--tol-scens", type=int, default=10000, help="scenarios of the PH-to-tol run")
     ap.add_argument("--crops", type=int, default=1)
     ap.add_argument("--rho", type=float, default=1.0)
     ap.add_argument("--tol-run", type=int, default=1, help="also time PH to convthresh")
@@ -127,7 +153,7 @@ def run():
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
 
-    S, c = args.scens, args.crops
+    S, c = args.scens * world, args.crops  # weak scaling: --scens per rank
     names = [f"scen{i}" for i in range(S)]
     opts = {"solvername": "mi355x_pdhg", "PHIterLimit": args.warmup + args.steps,
             "defaultPHrho": args.rho, "convthresh": -1.0, "verbose": False,
@@ -146,7 +172,6 @@ def run():
     ph.run_device_loop(0, args.warmup, -1.0, chunk=args.steps)
     b = ph.batch
     ph.solve_log.clear()
-    st0 = b.loop_status()
     # timed region: exactly `steps` PH iterations
     if world > 1:
         dist.barrier()
@@ -162,9 +187,11 @@ def run():
     if world > 1:
         dist.all_reduce(dts, op=dist.ReduceOp.MAX)
     dt = float(dts.item())
+    # (run_device_loop resets the device counters: st1 counts the timed steps)
     n_solves = st1[3]
     tot_iters = float(st1[4])
     n_polished = float(st1[6])
+    n_cached = float(st1[7])
 
     # kernel times: the next `steps` iterations of the same run, launched
     # eagerly with HIP events around the solve's kernels (library side, on
@@ -174,33 +201,39 @@ def run():
     ph.run_device_loop(args.warmup + args.steps, args.warmup + 2 * args.steps, -1.0,
                        chunk=args.steps)
     n_t, as_ms, po_ms, pd_ms = b.read_timing()
+    sb_ = b.loop_status()
     b.set_timing(False)
     ph.PHoptions["device_loop_graphs"] = True
-    as_ms /= max(n_t, 1)
-    po_ms /= max(n_t, 1)
-    pd_ms /= max(n_t, 1)
+    nt = max(n_t, 1)
+    as_ms, po_ms, pd_ms = as_ms / nt, po_ms / nt, pd_ms / nt
+    t_iters = float(sb_[4]) / nt              # PDHG steps per solve call (all scenarios)
+    t_pol = float(sb_[6]) / nt                # scenarios finished by a polish per call
+    t_pdhg = float(sb_[3] - sb_[6] - sb_[7]) / nt  # scenarios left to PDHG per call
 
     S_loc = ph.S_loc
     K = 3 * c
     n, m, nnz = farmer_dims(c)
-    # algorithmic HBM bytes of one active-set kernel launch: per scenario the
-    # cache entry (K keys + (K+1) x 2(n+m) affine map), the static block
-    # (4n+3m), W/rho/xbar (3K) and the validity flag in; x, y, status,
-    # iters, pobj, dbound and 5 diagnostics out
-    as_bytes = S_loc * (8 * (K + (K + 1) * 2 * (n + m) + 4 * n + 3 * m + 3 * K)
-                        + 4 + 8 * (n + m) + 8 + 16 + 40)
-    # PDHG kernel: every scenario's data in and solution out for the
-    # scenarios it solves + SURVEY 8(d) B_it per PDHG step taken
-    pd_scen = float(S_loc)  # upper bound: it may touch every scenario
-    if pd_ms >= as_ms:
-        kname, kms = "pdhg_kernel", pd_ms
-        kbytes = pd_scen * solve_bytes_per_scenario(c) + tot_iters / args.steps * bytes_per_pdhg_iter(c)
-    else:
-        kname, kms = "active_set_kernel", as_ms
-        kbytes = as_bytes
-    achieved_gbs = kbytes / (kms / 1000.0) / 1e9
+    cw = K + (K + 1) * 2 * (n + m)           # cache entry (doubles)
+    sbw = 4 * n + 3 * m                      # static block (doubles)
+    out_b = 8 * (n + m) + 4 + 4 + 16 + 40    # x, y, status, iters, pobj+dbound, diag
+    # algorithmic bytes per launch (what the kernel must move at least):
+    # active_set_kernel: every scenario's cache entry, static block,
+    #   W/rho/xbar and flag in, the solution out
+    as_bytes = S_loc * (8 * (cw + sbw + 3 * K) + 4 + out_b)
+    # polish_kernel: per miss the static block, W/rho/xbar, hint, matrix
+    #   values in; the solution and the refreshed cache entry out
+    po_bytes = t_pol * (8 * (sbw + 3 * K + 4 + nnz + cw) + out_b)
+    # pdhg_kernel: per scenario it solves the data in and the solution out
+    #   + SURVEY 8(d) B_it per PDHG step
+    pd_bytes = t_pdhg * solve_bytes_per_scenario(c) + t_iters * bytes_per_pdhg_iter(c)
+    cand = [("active_set_kernel", as_ms, as_bytes), ("polish_kernel", po_ms, po_bytes),
+            ("pdhg_kernel", pd_ms, pd_bytes)]
+    kname, kms, kbytes = max(cand, key=lambda t: t[1])
+    achieved_gbs = kbytes / (kms / 1000.0) / 1e9 if kms > 0 else 0.0
     mean_iters = tot_iters / max(n_solves, 1)
     polished_frac = n_polished / max(n_solves, 1)
+    cached_frac = n_cached / max(n_solves, 1)
+    traffic, traffic_src = pmc_traffic(kname, S_loc, c)
 
     # PH wall-clock to convergence tolerance (fresh run, same instance)
     tol_info = None
@@ -208,7 +241,8 @@ def run():
         opts2 = dict(opts)
         opts2["convthresh"] = args.convthresh
         opts2["PHIterLimit"] = 5000
-        ph2 = PH(opts2, names, farmer.scenario_creator,
+        names2 = [f"scen{i}" for i in range(args.tol_scens)]
+        ph2 = PH(opts2, names2, farmer.scenario_creator,
                  scenario_creator_kwargs={"crops_multiplier": c})
         ph2.PH_Prep()
         ph2.subproblem_creation()
@@ -227,7 +261,8 @@ def run():
         eobj = ph2.post_loops()
         tol_info = {"seconds": round(float(w.item()), 4), "ph_iterations": ph2._PHIter,
                     "convthresh": args.convthresh, "final_conv": ph2.conv,
-                    "trivial_bound": tb, "Eobj": eobj}
+                    "trivial_bound": tb, "Eobj": eobj, "scenarios": args.tol_scens,
+                    "n_gpus": world}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -250,33 +285,35 @@ def run():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1000.0, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (reference farmer generator, examples/farmer/farmer.py)",
-            "config": {"workload": f"farmer PH, {S} scenarios, crops_multiplier={c} "
+            "config": {"workload": f"farmer PH, {S} scenarios ({args.scens} per GPU), crops_multiplier={c} "
                                    f"(n={n}, m={m}, nnz={nnz} per scenario), rho={args.rho}, "
                                    f"prox-QP to 1e-9 rel KKT, warm-started",
-                       "scenarios": S, "crops_multiplier": c,
+                       "scenarios": S, "scenarios_per_gpu": args.scens, "crops_multiplier": c,
                        "parallelism": f"scenario-sharded x{world} (one rank per GPU, RCCL allreduce)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                         "traffic": None,
+                         "traffic": traffic,
                          "kernel": kname,
                          "kernel_ms": round(kms, 4),
-                         "alg_bytes_per_launch": kbytes,
-                         "kernels_ms": {"active_set_kernel": round(as_ms, 4),
-                                        "polish_kernel": round(po_ms, 4),
-                                        "pdhg_kernel": round(pd_ms, 4)},
-                         "note": "per-launch averages from HIP events on the launch stream over "
-                                 "the `steps` PH iterations that follow the timed region (same "
-                                 "run, eager launches). active_set_kernel bytes = per scenario the "
-                                 "cache entry + static block + W/rho/xbar in, solution out; "
-                                 "pdhg_kernel (misses of the cached active set: warm polish / "
-                                 "PDHG) bytes = every scenario's data in and solution out + "
-                                 "SURVEY 8(d) B_it x PDHG steps"},
+                         "alg_bytes_per_launch": round(kbytes),
+                         "kernels": {k: {"ms": round(t, 4), "alg_bytes": round(bb),
+                                         "GBps": round(bb / (t / 1000.0) / 1e9, 1) if t > 0 else None}
+                                     for k, t, bb in cand},
+                         "traffic_source": traffic_src,
+                         "note": "per-launch averages from HIP events recorded by the library on "
+                                 "the launch stream, over the `steps` PH iterations that follow "
+                                 "the timed region (same run, eager launches); the dominant "
+                                 "kernel by time is reported.  Algorithmic bytes: see DESIGN.md "
+                                 "section 6 (active_set: per scenario cache entry + static block "
+                                 "+ W/rho/xbar in, solution out; polish: per cache miss; pdhg: per "
+                                 "PDHG solve + SURVEY 8(d) B_it per PDHG step)."},
             "pdhg_iters_per_solve": round(mean_iters, 2),
             "polished_fraction": round(polished_frac, 4),
+            "cached_fraction": round(cached_frac, 4),
             "ph_to_tol": tol_info,
             "cpu_baseline": cpu,
         }

@@ -163,7 +163,8 @@ int ph_eval_objective(ph_batch_t b, const double *x, const double *W,
  * Diagnostics of the last ph_pdhg_solve, copied to host out[PH_DIAG_W*S]:
  * per scenario the final relative primal residual, dual residual, duality
  * gap, Halpern fixed-point residual and how the solve ended (0 PDHG reached
- * tol, 1 active-set polish of the warm start, 2 polish of a PDHG iterate)
+ * tol, 1 active-set polish of the warm start, 2 polish of a PDHG iterate,
+ * 3 the cached active set's affine map)
  * (synchronises the stream).
  */
 int ph_batch_get_diag(ph_batch_t b, double *out /*host [S][PH_DIAG_W]*/);
@@ -172,11 +173,12 @@ int ph_batch_get_diag(ph_batch_t b, double *out /*host [S][PH_DIAG_W]*/);
  * Summary of the last ph_pdhg_solve, copied to host (synchronises the
  * stream): out[0] scenarios not solved to tolerance (status != optimal),
  * out[1] PDHG iterations summed over scenarios, out[2] the largest count,
- * out[3] scenarios finished by the active-set polish.  One small copy
+ * out[3] scenarios finished by an active-set polish (how 1 or 2), out[4]
+ * scenarios finished by the active-set cache (how 3).  One small copy
  * replaces reading status[S] after every solve (phbase.py:959-965 checks
  * each scenario's status).
  */
-int ph_batch_solve_summary(ph_batch_t b, int64_t *out /*host [4]*/);
+int ph_batch_solve_summary(ph_batch_t b, int64_t *out /*host [5]*/);
 
 /*
  * Device-side PH iteration control (iterk_loop without a host round trip
@@ -202,7 +204,7 @@ int ph_batch_solve_summary(ph_batch_t b, int64_t *out /*host [4]*/);
  * host computes the Compute_Xbar sums once (ph_xbar_accum).  ph_loop_enable
  * switches the flag checks on / off; ph_loop_status copies {stop, iter,
  * not-optimal solves, solves, PDHG iterations (sum), PDHG iterations (max),
- * polished} to host out[7] (synchronises).
+ * polished, cached} to host out[8] (synchronises).
  */
 int ph_loop_reset(ph_batch_t b, int32_t start_iter, int32_t iter_limit,
                   double convthresh);
@@ -217,7 +219,7 @@ int ph_loop_conv_local(ph_batch_t b, const double *absdiff /*dev [S]*/,
                        const int32_t *seg /*dev [R+1]*/, int32_t R,
                        const double *cnt /*dev [R]*/, double nproc,
                        double *parts /*dev [R] out*/, double *conv_hist);
-int ph_loop_status(ph_batch_t b, int64_t *out /*host [7]*/);
+int ph_loop_status(ph_batch_t b, int64_t *out /*host [8]*/);
 
 /*
  * Kernel timing of ph_pdhg_solve with HIP events recorded on the batch's

@@ -262,7 +262,7 @@ struct LoopCtl {
   int32_t limit;  // PHIterLimit
   int32_t pad;
   double thresh;  // convthresh
-  unsigned long long acc[5];  // not optimal, solves, iters sum, iters max, polished
+  unsigned long long acc[6];  // not optimal, solves, iters sum, iters max, polished, cached
 };
 
 __device__ __forceinline__ bool stopped(const LoopCtl *c) {
@@ -1967,7 +1967,8 @@ __global__ void __launch_bounds__(1024) segment_sum_kernel(
   if (threadIdx.x == 0) out[r] = acc[0];
 }
 
-// One block: (not optimal, sum iters, max iters, polished) of the last solve.
+// Block 0: (not optimal, sum iters, max iters, polished, cached) of the last
+// solve (polished: how 1/2, cached: how 3).
 // A reduction instead of per-workgroup atomics on one address, which
 // serialise 10k+ workgroups at the end of the solve.
 __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__restrict__ status,
@@ -1975,13 +1976,13 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
                                                        const double *__restrict__ diag,
                                                        unsigned long long *__restrict__ out,
                                                        LoopCtl *ctl, XbarArgs xa) {
-  __shared__ unsigned long long red[4][MAX_WAVES];
+  __shared__ unsigned long long red[5][MAX_WAVES];
   if (stopped(ctl)) return;
   if (blockIdx.x > 0) {  // device loop: next iteration's Compute_Xbar sums
     xbar_sums_block(xa, blockIdx.x - 1);
     return;
   }
-  unsigned long long v[4] = {0ull, 0ull, 0ull, 0ull};
+  unsigned long long v[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
   const int bd = blockDim.x;
   for (int s0 = threadIdx.x; s0 < S; s0 += 4 * bd) {
     int st[4], itr[4];
@@ -1999,24 +2000,25 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
       v[0] += st[u] != PH_STATUS_OPTIMAL;
       v[1] += it;
       v[2] = it > v[2] ? it : v[2];
-      v[3] += hw[u] != 0.0;
+      v[3] += hw[u] == 1.0 || hw[u] == 2.0;
+      v[4] += hw[u] == 3.0;
     }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 5; ++i) {
       const unsigned long long o = __shfl_xor(v[i], off, WAVE);
       v[i] = i == 2 ? (o > v[i] ? o : v[i]) : v[i] + o;
     }
   }
   const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
   if (lane == 0)
-    for (int i = 0; i < 4; ++i) red[i][wid] = v[i];
+    for (int i = 0; i < 5; ++i) red[i][wid] = v[i];
   __syncthreads();
   if (threadIdx.x == 0) {
     const int nw = blockDim.x / WAVE;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 5; ++i) {
       unsigned long long t = red[i][0];
       for (int w = 1; w < nw; ++w) t = i == 2 ? (red[i][w] > t ? red[i][w] : t) : t + red[i][w];
       out[i] = t;
@@ -2027,6 +2029,7 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
       ctl->acc[2] += out[1];
       ctl->acc[3] = out[2] > ctl->acc[3] ? out[2] : ctl->acc[3];
       ctl->acc[4] += out[3];
+      ctl->acc[5] += out[4];
       loop_advance(ctl);
     }
   }
@@ -2215,7 +2218,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
       (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
-      (rc = dalloc(&b->d_summary, 4)) || (rc = dalloc(&b->d_ctr, 4)) || (rc = dalloc(&b->d_ctl, 1)) ||
+      (rc = dalloc(&b->d_summary, 5)) || (rc = dalloc(&b->d_ctr, 4)) || (rc = dalloc(&b->d_ctl, 1)) ||
       (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
@@ -2505,10 +2508,10 @@ int ph_batch_get_diag(ph_batch_t b, double *out) {
 
 int ph_batch_solve_summary(ph_batch_t b, int64_t *out) {
   if (!b || !out) return fail(PH_EINVAL, "ph_batch_solve_summary: bad arguments");
-  unsigned long long h[4];
+  unsigned long long h[5];
   HIP_OK(hipMemcpyAsync(h, b->d_summary, sizeof(h), hipMemcpyDeviceToHost, b->stream));
   HIP_OK(hipStreamSynchronize(b->stream));
-  for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
+  for (int i = 0; i < 5; ++i) out[i] = (int64_t)h[i];
   return PH_OK;
 }
 
@@ -2581,6 +2584,7 @@ int ph_loop_status(ph_batch_t b, int64_t *out) {
   out[4] = (int64_t)h.acc[2];
   out[5] = (int64_t)h.acc[3];
   out[6] = (int64_t)h.acc[4];
+  out[7] = (int64_t)h.acc[5];
   return PH_OK;
 }
 

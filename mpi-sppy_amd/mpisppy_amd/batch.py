@@ -189,7 +189,7 @@ class DeviceBatch:
         self.pobj = torch.zeros(self.S, **f64)
         self.dbound = torch.zeros(self.S, **f64)
         self.const = up(data.const)
-        self._summary = np.zeros(4, dtype=np.int64)
+        self._summary = np.zeros(5, dtype=np.int64)
         self.time_kernel = False  # record HIP events around each solve launch
         self._events = None
         self.event_log = []       # every (start, end) event pair recorded
@@ -237,8 +237,8 @@ class DeviceBatch:
         return [e0.elapsed_time(e1) for e0, e1 in self.event_log]
 
     def summary(self):
-        """(not optimal, sum of PDHG iterations, max iterations, polished) of the
-        last solve; synchronises the stream (one 32-byte copy)."""
+        """(not optimal, sum of PDHG iterations, max iterations, polished, cached)
+        of the last solve; synchronises the stream (one 40-byte copy)."""
         _native.check(self.lib.ph_batch_solve_summary(
             self.handle, self._summary.ctypes.data_as(_native._c_ptr)), "ph_batch_solve_summary")
         return tuple(int(v) for v in self._summary)
@@ -280,9 +280,9 @@ class DeviceBatch:
                                             _native.ptr(conv_hist)), "ph_loop_conv")
 
     def loop_status(self):
-        """(stop, iter, not-optimal solves, solves, PDHG iters sum, max, polished);
-        synchronises.  stop: 0 running, 1 converged, 2 iteration limit."""
-        out = np.zeros(7, dtype=np.int64)
+        """(stop, iter, not-optimal solves, solves, PDHG iters sum, max, polished,
+        cached); synchronises.  stop: 0 running, 1 converged, 2 iteration limit."""
+        out = np.zeros(8, dtype=np.int64)
         _native.check(self.lib.ph_loop_status(self.handle, out.ctypes.data_as(_native._c_ptr)),
                       "ph_loop_status")
         return tuple(int(v) for v in out)
@@ -311,7 +311,8 @@ class DeviceBatch:
 
     def diagnostics(self):
         """[S][5] host array: final (primal res, dual res, gap, fixed-point res,
-        how: 0 PDHG tol, 1 warm-start polish, 2 polish of a PDHG iterate)."""
+        how: 0 PDHG tol, 1 warm-start polish, 2 polish of a PDHG iterate,
+        3 active-set cache)."""
         out = np.zeros((self.S, _native.DIAG_W))
         _native.check(self.lib.ph_batch_get_diag(self.handle, out.ctypes.data_as(_native._c_ptr)),
                       "ph_batch_get_diag")

@@ -233,9 +233,10 @@ class PHBase(SPBase):
         b = self.batch
         t0 = time.perf_counter()
         b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
-        nonopt, it_sum, it_max, npol = b.summary()  # waits for the solve
+        nonopt, it_sum, it_max, npol, ncache = b.summary()  # waits for the solve
         dt = time.perf_counter() - t0
-        self.solve_log.append((self.S_loc, dt, it_sum / max(self.S_loc, 1), it_max, npol))
+        self.solve_log.append((self.S_loc, dt, it_sum / max(self.S_loc, 1), it_max,
+                               npol + ncache))
         if nonopt:
             status = b.status.cpu().numpy()
             self.scenario_feasible = (status == 0) | (status == 1)
@@ -494,7 +495,8 @@ class PHBase(SPBase):
                         self._device_iteration(kw)
                 st = b.loop_status()
                 dt = time.perf_counter() - t0
-                stop, it, nonopt, nsolves, it_sum, it_max, npol = st
+                stop, it, nonopt, nsolves, it_sum, it_max, npol, ncache = st
+                npol += ncache
                 prev = getattr(self, "_loop_prev", (0, 0))
                 self._loop_prev = (nsolves, npol)
                 if nsolves > prev[0]:

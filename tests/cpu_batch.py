@@ -39,7 +39,7 @@ class CPUBatch:
 
     def loop_reset(self, start_iter, iter_limit, convthresh):
         self._ctl = dict(stop=0, iter=int(start_iter), limit=int(iter_limit),
-                         thresh=float(convthresh), acc=[0, 0, 0, 0, 0])
+                         thresh=float(convthresh), acc=[0, 0, 0, 0, 0, 0])
         self._advance()
 
     def _advance(self):
@@ -114,7 +114,7 @@ class CPUBatch:
     def summary(self):
         st = self.status.numpy()
         it = self.iters.numpy()
-        return int(np.sum(st != 0)), int(it.sum()), int(it.max(initial=0)), 0
+        return int(np.sum(st != 0)), int(it.sum()), int(it.max(initial=0)), 0, 0
 
     def xbar_accum(self, prob_coeff, slot_k, slot_s0, slot_s1, out):
         if self._stopped():
