@@ -1349,52 +1349,72 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Copy `len` contiguous doubles to LDS with one wave: all loads of a batch of
-// four per lane issued before any store (one memory round trip per 256).
-__device__ __forceinline__ void wave_stage(double *dst, const double *__restrict__ src, int len,
-                                           int lane) {
+// Two contiguous ranges to LDS with one wave, all loads of a batch (four
+// per lane per range) issued before any store.
+__device__ __forceinline__ void wave_stage2(double *d1, const double *__restrict__ s1, int l1,
+                                            double *d2, const double *__restrict__ s2, int l2,
+                                            int lane) {
+  const int len = l1 > l2 ? l1 : l2;
   for (int q0 = 0; q0 < len; q0 += 4 * WAVE) {
-    double t[4];
+    double t1[4], t2[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int q = q0 + u * WAVE + lane;
-      t[u] = q < len ? src[q] : 0.0;
+      t1[u] = q < l1 ? s1[q] : 0.0;
+      t2[u] = q < l2 ? s2[q] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int q = q0 + u * WAVE + lane;
-      if (q < len) dst[q] = t[u];
+      if (q < l1) d1[q] = t1[u];
+      if (q < l2) d2[q] = t2[u];
     }
   }
 }
 
-template <int WPB>
+// One wave evaluates SPW consecutive scenarios: their entries and static
+// blocks are contiguous, so they stage in one round of coalesced loads.
+template <int WPB, int SPW>
 __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x / WAVE;
-  const int s = blockIdx.x * WPB + w;
-  if (s >= a.S || stopped(a.ctl)) return;  // wave-uniform; no block barriers
+  const int sw = (blockIdx.x * WPB + w) * SPW;
+  if (sw >= a.S || stopped(a.ctl)) return;  // wave-uniform; no block barriers
   const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m);
   const int SBW = 4 * n + 3 * m;
-  // ---- the scenario's cache entry and static block, staged through LDS by
-  // coalesced loads (one round trip), plus the PH terms and the flag
-  double *ent = lds + (size_t)w * (a.CW + SBW + WAVE);
-  double *sb = ent + a.CW;
-  double *xsw = sb + SBW;  // [WAVE] scratch for the clipped case
-  const int ok = a.cache_ok[s];
-  double hk_l = 0.0, qk_l = 0.0, cst_l = 0.0;
-  if (lane < K) {
-    const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
-    const double xb = a.xbar[(size_t)lane * S + s];
-    hk_l = a.w_on * W - a.prox_on * r * xb;
-    qk_l = a.prox_on * r;
-    cst_l = a.prox_on * 0.5 * r * xb * xb;
+  const int ns = (a.S - sw) < SPW ? (a.S - sw) : SPW;  // scenarios of this wave
+  double *ent0 = lds + (size_t)w * (SPW * (a.CW + SBW) + WAVE);
+  double *sb0 = ent0 + SPW * a.CW;
+  double *xsw = sb0 + SPW * SBW;  // [WAVE] scratch for the clipped case
+  // ---- everything of the wave's scenarios in one round of loads
+  int okv[SPW];
+  double hkv[SPW], qkv[SPW], cstv[SPW];
+#pragma unroll
+  for (int u = 0; u < SPW; ++u) {
+    const int s = sw + u;
+    okv[u] = u < ns ? a.cache_ok[s] : 0;
+    hkv[u] = qkv[u] = cstv[u] = 0.0;
+    if (u < ns && lane < K) {
+      const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
+      const double xb = a.xbar[(size_t)lane * S + s];
+      hkv[u] = a.w_on * W - a.prox_on * r * xb;
+      qkv[u] = a.prox_on * r;
+      cstv[u] = a.prox_on * 0.5 * r * xb * xb;
+    }
   }
   const int kslot = lane < n ? a.slot_of_col[lane] : -1;
-  wave_stage(ent, a.cache + (size_t)s * a.CW, a.CW, lane);
-  wave_stage(sb, a.sb + (size_t)s * SBW, SBW, lane);
+  wave_stage2(ent0, a.cache + (size_t)sw * a.CW, ns * a.CW, sb0, a.sb + (size_t)sw * SBW,
+              ns * SBW, lane);
   wsync();
+#pragma unroll
+  for (int u = 0; u < SPW; ++u) {
+  if (u >= ns) break;
+  const int s = sw + u;
+  const int ok = okv[u];
+  const double hk_l = hkv[u], qk_l = qkv[u], cst_l = cstv[u];
+  const double *ent = ent0 + (size_t)u * a.CW;
+  const double *sb = sb0 + (size_t)u * SBW;
   const double *B = ent + K;
   double DC = 1.0, G = 0.0, L = 0.0, U = 0.0, XU = 0.0, ATY = 0.0;
   if (lane < n) {
@@ -1439,7 +1459,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
       a.hint_ok[s] = 0;
       a.wl[atomicAdd(a.wl_count, 1)] = s;
     }
-    return;
+    continue;
   }
   double XN = lane < n ? clampd(XU, L, U) : 0.0;
   const double YN = YU;
@@ -1472,7 +1492,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
       a.hint_ok[s] = 1;
       a.wl[atomicAdd(a.wl_count, 1)] = s;
     }
-    return;
+    continue;
   }
   if (lane < n) a.x[(size_t)lane * S + s] = XN * DC;
   if (lane < m) a.y[(size_t)lane * S + s] = YN * DR;
@@ -1488,6 +1508,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
     dg[3] = -1.0;
     dg[4] = 3.0;
   }
+  }  // scenarios of the wave
 }
 
 // Start the next iteration (phbase.py:1498 loop head): count it, or stop
@@ -1563,8 +1584,10 @@ __global__ void __launch_bounds__(1024) loop_conv_local_kernel(
 // K > RG_K) go to pdhg_kernel directly.
 // ------------------------------------------------------------------------
 constexpr int RG_W = 32;               // register row width
-constexpr int RG_K = 8;                // parametric right-hand sides
+constexpr int RG_K = 4;                // parametric right-hand sides
 constexpr int RG_R0 = RG_W - 1 - RG_K; // first right-hand-side column = max unknowns
+// LDS staging: the KKT rows, later the 1+K product vectors (x and y parts)
+constexpr int RG_KST = (RG_R0 * RG_W > 2 * (1 + RG_K) * WAVE) ? RG_R0 * RG_W : 2 * (1 + RG_K) * WAVE;
 
 template <int CTRL>
 __device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
@@ -1604,8 +1627,8 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
   const int count = stopped(a.ctl) ? 0 : *a.wl_count;
   if ((int)blockIdx.x >= count) return;
   // LDS: staging rows | solutions | vals | xs | ys | pattern + maps
-  double *kst = lds;                        // [RG_R0][RG_W]
-  double *sol = kst + RG_R0 * RG_W;         // [1+RG_K][WAVE]
+  double *kst = lds;                        // [RG_KST]: staging rows / product vectors
+  double *sol = kst + RG_KST;               // [1+RG_K][WAVE]
   double *vl = sol + (1 + RG_K) * WAVE;     // [nnz]
   double *xs = vl + nnz;                    // [WAVE]
   double *ys = xs + WAVE;                   // [WAVE]
@@ -1704,8 +1727,8 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
         xs[lane] = xfix;
       }
       if (lane < m) rpos[lane] = ac ? pR : -1;
-      for (int q = lane; q < RG_R0 * RG_W; q += WAVE) kst[q] = 0.0;
-      for (int q = lane; q < (1 + RG_K) * WAVE; q += WAVE) sol[q] = 0.0;
+      for (int q = lane; q < N * RG_W; q += WAVE) kst[q] = 0.0;
+      for (int q = lane; q < (1 + K) * WAVE; q += WAVE) sol[q] = 0.0;
       __syncthreads();
       if (fr) {  // stationarity row of free column `lane`
         double *row = kst + pF * RG_W;
@@ -1803,33 +1826,57 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
         if (a.cache) {
           double *cs = a.cache + (size_t)s * a.CW;
           const int VL = cache_vlen(n, m);
+          // the 1+K vectors (u at this h, then d u / d h_k) to LDS, their
+          // products with A and A' in one pass over the pattern
+          double *xk = kst, *yk = kst + (1 + RG_K) * WAVE;
           __syncthreads();
-          if (lane < n) xs[lane] = XU;
-          if (lane < m) ys[lane] = YU;
+#pragma unroll
+          for (int t = 0; t <= RG_K; ++t) {
+            if (t <= K) {
+              xk[t * WAVE + lane] = lane < n ? (t == 0 ? XU : (fr ? sol[t * WAVE + pF] : 0.0)) : 0.0;
+              yk[t * WAVE + lane] = lane < m ? (t == 0 ? YU : (ac ? sol[t * WAVE + pR] : 0.0)) : 0.0;
+            }
+          }
           __syncthreads();
-          double bx = XU, by = YU, bax = rowdot(), baty = coldot();
-          for (int k = 0; k < K; ++k) {
-            const double hk = __shfl(hk_l, k, WAVE);
-            const double dx = fr ? sol[(k + 1) * WAVE + pF] : 0.0;
-            const double dy = ac ? sol[(k + 1) * WAVE + pR] : 0.0;
-            __syncthreads();
-            if (lane < n) xs[lane] = dx;
-            if (lane < m) ys[lane] = dy;
-            __syncthreads();
-            const double dax = rowdot(), daty = coldot();
-            double *Dk = cs + K + (size_t)(k + 1) * VL;
-            if (lane < n) {
-              Dk[cv_x(n, m) + lane] = dx;
-              Dk[cv_aty(n, m) + lane] = daty;
+          double pax[1 + RG_K], paty[1 + RG_K];
+#pragma unroll
+          for (int t = 0; t <= RG_K; ++t) pax[t] = paty[t] = 0.0;
+          if (lane < m)
+            for (int p = rp[lane]; p < rp[lane + 1]; ++p) {
+              const int j = ci[p];
+              const double av = vl[p];
+#pragma unroll
+              for (int t = 0; t <= RG_K; ++t)
+                if (t <= K) pax[t] = fma(av, xk[t * WAVE + j], pax[t]);
             }
-            if (lane < m) {
-              Dk[cv_y(n, m) + lane] = dy;
-              Dk[cv_ax(n, m) + lane] = dax;
+          if (lane < n)
+            for (int p = cp[lane]; p < cp[lane + 1]; ++p) {
+              const int i = cr[p];
+              const double av = vl[ck[p]];
+#pragma unroll
+              for (int t = 0; t <= RG_K; ++t)
+                if (t <= K) paty[t] = fma(av, yk[t * WAVE + i], paty[t]);
             }
-            bx -= hk * dx;
-            by -= hk * dy;
-            bax -= hk * dax;
-            baty -= hk * daty;
+          double bx = XU, by = YU, bax = pax[0], baty = paty[0];
+#pragma unroll
+          for (int t = 1; t <= RG_K; ++t) {
+            if (t <= K) {
+              const double hk = __shfl(hk_l, t - 1, WAVE);
+              const double dx = xk[t * WAVE + lane], dy = yk[t * WAVE + lane];
+              double *Dk = cs + K + (size_t)t * VL;
+              if (lane < n) {
+                Dk[cv_x(n, m) + lane] = dx;
+                Dk[cv_aty(n, m) + lane] = paty[t];
+              }
+              if (lane < m) {
+                Dk[cv_y(n, m) + lane] = dy;
+                Dk[cv_ax(n, m) + lane] = pax[t];
+              }
+              bx -= hk * dx;
+              by -= hk * dy;
+              bax -= hk * pax[t];
+              baty -= hk * paty[t];
+            }
           }
           double *B = cs + K;
           const int jk = lane < K ? a.nonant_col[lane] : 0;
@@ -2260,7 +2307,7 @@ static size_t scale_lds_bytes(const ph_batch *b) {
 }
 constexpr int POLISH_GRID = 2048;  // polish_kernel blocks (one wave each)
 static size_t polish_lds_bytes(const ph_batch *b) {
-  return sizeof(double) * ((size_t)RG_R0 * RG_W + (1 + RG_K) * WAVE + b->nnz + 2 * WAVE) +
+  return sizeof(double) * ((size_t)RG_KST + (1 + RG_K) * WAVE + b->nnz + 2 * WAVE) +
          sizeof(int32_t) * ((size_t)(b->m + 1) + 3 * (size_t)b->nnz + (b->n + 1) + 2 * WAVE);
 }
 static bool polish_fits(const ph_batch *b) {
@@ -2339,7 +2386,7 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
   // active-set cache: for polish-size scenarios whose entry (+ static
   // block) stages in a quarter of the LDS per 4-wave block
   const size_t cw = (size_t)K + (K + 1) * 2 * (size_t)(b->n + b->m);
-  if (polish_fits(b) && 4 * 8 * (cw + 4 * b->n + 3 * b->m + WAVE) <= 40 * 1024) {
+  if (polish_fits(b) && 4 * 8 * (2 * (cw + 4 * b->n + 3 * b->m) + WAVE) <= 40 * 1024) {
     b->CW = (int)cw;
     if ((rc = dalloc(&b->d_cache, (size_t)b->S * b->CW)) || (rc = dalloc(&b->d_cache_ok, b->S)) ||
         (rc = dalloc(&b->d_hint, (size_t)b->S * 4)) || (rc = dalloc(&b->d_hint_ok, b->S)) ||
@@ -2421,11 +2468,13 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     a.hint = b->d_hint;
     a.hint_ok = b->d_hint_ok;
     a.wl = b->d_wl;
-    constexpr int WPB = 4;
+    constexpr int WPB = 4, SPW = 1;
     a.wl2 = b->d_wl2;
-    const size_t as_lds = sizeof(double) * WPB * ((size_t)b->CW + 4 * b->n + 3 * b->m + WAVE);
-    hipLaunchKernelGGL((active_set_kernel<WPB>), dim3((b->S + WPB - 1) / WPB), dim3(WPB * WAVE),
-                       as_lds, b->stream, a);
+    const size_t as_lds =
+        sizeof(double) * WPB * (SPW * ((size_t)b->CW + 4 * b->n + 3 * b->m) + WAVE);
+    const int per_block = WPB * SPW;
+    hipLaunchKernelGGL((active_set_kernel<WPB, SPW>), dim3((b->S + per_block - 1) / per_block),
+                       dim3(WPB * WAVE), as_lds, b->stream, a);
     HIP_OK(hipGetLastError());
     if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
     // the misses: register Gauss-Jordan polish; what it cannot finish goes
