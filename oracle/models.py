@@ -225,3 +225,67 @@ def hydro(scenario_name, branching_factors=(3, 3)):
     nodes = [("ROOT", 1.0, [Pgt(0), Pgh(0), PDns(0), Vol(0)]),
              (ndn, 1.0 / bf[0], [Pgt(1), Pgh(1), PDns(1), Vol(1)])]
     return OScen(scenario_name, names, c, sp.csr_matrix(Am), rl, ru, l, u, nodes)
+
+
+# ------------------------------------------------------------------ sslp ----
+# examples/sslp/model/ReferenceModel.py:22-94 (LP relaxation: binaries in
+# [0, 1]), scenario_creator sslp.py:17-33.  Instance data: the reference's
+# data/<inst>/scenariodata/Scenario*.dat, converted to JSON by
+# tools/make_sslp_data.py (mpi-sppy_amd/mpisppy_amd/examples/data/sslp.json).
+_SSLP_JSON = None
+
+
+def _sslp_json():
+    global _SSLP_JSON
+    if _SSLP_JSON is None:
+        import json
+        import os
+        here = os.path.dirname(os.path.abspath(__file__))
+        path = os.path.join(here, "..", "mpi-sppy_amd", "mpisppy_amd", "examples", "data", "sslp.json")
+        with open(path) as f:
+            _SSLP_JSON = json.load(f)
+    return _SSLP_JSON
+
+
+def sslp(scenario_name, instance="sslp_15_45_5"):
+    d = _sslp_json()
+    snum = extract_num(scenario_name)
+    m_ = re.fullmatch(r"sslp_(\d+)_(\d+)_synthetic", instance)
+    if m_:
+        size = d["sizes"][f"{m_.group(1)}_{m_.group(2)}"]
+        present = (np.random.RandomState(1134 + snum).rand(size["NumClients"]) < 0.5) * 1.0
+    else:
+        inst = d["instances"][instance]
+        size = d["sizes"][inst["size"]]
+        present = np.asarray(inst["ClientPresent"][snum - 1], dtype=np.float64)
+    J, I = size["NumServers"], size["NumClients"]
+    dem = np.asarray(size["Demand"])          # [I][J]
+    rev = np.asarray(size["Revenue"])         # [I][J]
+    # variables: FacilityOpen[J], Allocation[I][J] (client major), Dummy[J]
+    n = J + I * J + J
+    yo = np.arange(J)
+    xa = (J + np.arange(I * J)).reshape(I, J)
+    du = J + I * J + np.arange(J)
+    A = np.zeros((J + I, n))
+    rl = np.zeros(J + I)
+    ru = np.zeros(J + I)
+    for j in range(J):          # demand_constraint_rule: sum_i d x - u_j - cap y_j <= 0
+        A[j, xa[:, j]] = dem[:, j]
+        A[j, du[j]] = -1.0
+        A[j, yo[j]] = -size["Capacity"]
+        rl[j], ru[j] = -np.inf, 0.0
+    for i in range(I):          # client_rule: sum_j x_ij = present_i
+        A[J + i, xa[i, :]] = 1.0
+        rl[J + i] = ru[J + i] = present[i]
+    c = np.zeros(n)
+    c[yo] = size["FixedCost"]
+    c[du] = 1000.0              # Penalty default
+    c[xa] = -rev
+    l = np.zeros(n)
+    u = np.ones(n)
+    u[du] = np.inf
+    names = ([f"FacilityOpen[{j + 1}]" for j in range(J)]
+             + [f"Allocation[{(i + 1, j + 1)}]" for i in range(I) for j in range(J)]
+             + [f"Dummy[{j + 1}]" for j in range(J)])
+    nodes = [("ROOT", 1.0, list(yo))]
+    return OScen(scenario_name, names, c, sp.csr_matrix(A), rl, ru, l, u, nodes)

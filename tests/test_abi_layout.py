@@ -123,3 +123,29 @@ def test_hydro_and_doc_farmer_layout_match_oracle():
         o = om.doc_farmer(nm)
         assert np.array_equal(_dense(bd, s), o.A.toarray())
         assert list(bd.nonant_cols) == list(o.nonant_idx)
+
+
+@pytest.mark.parametrize("inst", ["sslp_15_45_5", "sslp_5_25_50", "sslp_15_45_synthetic"])
+def test_sslp_layout_matches_oracle(inst):
+    """sslp LP relaxation: the batch builder, the per-scenario LinearModel
+    path and the oracle restatement give the same arrays."""
+    import scipy.sparse as sp
+    from mpisppy_amd.batch import from_models
+    from mpisppy_amd.examples import sslp
+    from oracle import models as om
+    names = sslp.scenario_names(4)
+    bd = sslp.batch_creator(names, instance=inst)
+    md = from_models(names, [sslp.scenario_creator(nm, instance=inst) for nm in names])
+    for a in ["row_ptr", "col_idx", "vals", "c", "l", "u", "rl", "ru", "nonant_cols"]:
+        assert np.array_equal(getattr(bd, a), getattr(md, a)), a
+    for s, nm in enumerate(names):
+        o = om.sslp(nm, inst)
+        A = sp.csr_matrix((bd.vals[:, s], bd.col_idx, bd.row_ptr), shape=(bd.m, bd.n)).toarray()
+        assert np.array_equal(A, o.A.toarray())
+        assert np.array_equal(bd.c[:, s], o.c)
+        assert np.array_equal(bd.rl[:, s], o.rl) and np.array_equal(bd.ru[:, s], o.ru)
+        assert np.array_equal(bd.l[:, s], o.l) and np.array_equal(bd.u[:, s], o.u)
+        assert list(bd.nonant_cols) == list(o.nonant_idx)
+    # data_dir form of the reference's scenario_creator (sslp.py:17-25)
+    m = sslp.scenario_creator("Scenario1", data_dir=f"data/{inst}/scenariodata")
+    assert m.num_vars == bd.n

@@ -112,3 +112,42 @@ def test_lagrangian_bound_matches_oracle():
     orc.ph_main()
     opsb = orc.post_solve_bound()
     assert abs(psb - opsb) / abs(opsb) < 1e-6
+
+
+def test_sslp_lp_relaxation_ph_matches_oracle():
+    """sslp_15_45_5 LP relaxation (705 columns, 60 rows, 1364 nonzeros per
+    scenario: the PDHG path with chunked rows).  No reference pin exists for
+    sslp (parity unpinned against the reference).  Its Iter0 LP has
+    alternative optima in FacilityOpen, so the PH trajectory depends on the
+    vertex a solver returns; checked against the oracle: the trivial bound
+    (unique), then PH prox-QP solves from the oracle's own PH states (W,
+    xbar after iterations 1 and 4), whose nonant optimum is unique."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import sslp
+    names = sslp.scenario_names(5)
+    opts = _opts(PHIterLimit=10, defaultPHrho=1.0, convthresh=1e-6)
+    ph = PH(dict(opts), names, sslp.scenario_creator,
+            scenario_creator_kwargs={"data_dir": "data/sslp_15_45_5/scenariodata"})
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    tb = ph.Iter0()
+    orc = OraclePH(dict(opts), [om.sslp(n, "sslp_15_45_5") for n in names])
+    ot = orc.Iter0()
+    assert abs(tb - ot) / abs(ot) < 1e-7
+    K, S = ph.K, ph.S_loc
+    for k in range(1, 5):
+        orc.Compute_Xbar()
+        orc.Update_W()
+        if k in (1, 4):
+            ph.W.copy_(torch.as_tensor(np.array(orc.W).T.reshape(-1), device=ph.W.device))
+            ph.xbar.copy_(torch.as_tensor(np.array(orc.xbar).T.reshape(-1), device=ph.W.device))
+            ph.solve_loop(solver_options=ph.current_solver_options)
+        orc.solve_loop()
+        if k in (1, 4):
+            x = ph.batch.x.view(ph.batch.n, S).cpu().numpy()
+            xn = x[ph.batch_data.nonant_cols]            # [K][S]
+            xo = np.array([orc.x[s][orc.scens[s].nonant_idx] for s in range(S)]).T
+            assert _rel(xn, xo) < 1e-6, (k, np.abs(xn - xo).max())
+            pobj = (ph.batch.pobj + ph.batch.const).cpu().numpy()
+            oobj = np.array([orc.objective(s) for s in range(S)])
+            assert _rel(pobj, oobj) < 1e-7, (k, pobj, oobj)

@@ -89,3 +89,21 @@ def test_farmer_yields_restate_reference_rng():
     got = [-s.A[7 + k, k] for k in range(6)]    # LimitAmountSold rows carry -Yield*DA
     assert np.allclose(got, expect)
     assert om.farmer("scen1", 1).A[1, 0] == 2.5   # groupnum 0: base yield, no draw
+
+
+def test_sslp_lp_relaxation_bounds():
+    """sslp_15_45_5 LP relaxation (no reference pin exists for sslp: parity
+    unpinned against the reference, checked for consistency here): the PH
+    trivial bound is a valid lower bound of the EF, Eobj after 10 PH
+    iterations is finite, and every prox-QP
+    solve passes the KKT check (the oracle raises otherwise)."""
+    from oracle.ef import solve_ef
+    names = [f"Scenario{i + 1}" for i in range(5)]
+    sc = [om.sslp(n, "sslp_15_45_5") for n in names]
+    ef_val, _ = solve_ef(sc)
+    orc = OraclePH({"PHIterLimit": 10, "defaultPHrho": 1.0, "convthresh": 1e-6}, sc)
+    conv, eobj, tb = orc.ph_main()
+    assert tb <= ef_val + 1e-9 * abs(ef_val)
+    assert abs(ef_val - (-280.4902709111119)) < 1e-6
+    assert abs(tb - (-291.989987012987)) < 1e-6
+    assert orc.iters == 10 and 0.0 < conv < 0.05
