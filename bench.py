@@ -112,6 +112,65 @@ def pmc_traffic(kname, S_loc, c):
     return None, None
 
 
+def hbm_config(args, world, farmer, PH, opts):
+    """F3: farmer c=--hbm-crops, --scens scenarios per rank.  Iter0, one
+    warmup iteration, then --hbm-steps PH iterations through the device loop
+    with the library's kernel events; the PDHG kernel's algorithmic bytes are
+    SURVEY 8(d) B_it per scenario-step x the steps taken + every scenario's
+    data in/out."""
+    c = args.hbm_crops
+    S = args.scens * world
+    names = [f"scen{i}" for i in range(S)]
+    o = dict(opts)
+    ph = PH(o, names, farmer.scenario_creator, scenario_creator_kwargs={"crops_multiplier": c})
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    ph._create_solvers()
+    b = ph.batch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ph.Iter0()
+    torch.cuda.synchronize()
+    t_iter0 = time.perf_counter() - t0
+    nonopt0 = b.summary()[0]
+    ph.run_device_loop(0, 1, -1.0, chunk=1)
+    ph.PHoptions["device_loop_graphs"] = False
+    b.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ph.run_device_loop(1, 1 + args.hbm_steps, -1.0, chunk=args.hbm_steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n_t, as_ms, po_ms, pd_ms = b.read_timing()
+    st = b.loop_status()
+    b.set_timing(False)
+    d = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    dt = float(d.item())
+    nt = max(n_t, 1)
+    pd_ms /= nt
+    steps_per_launch = st[4] / nt
+    pd_bytes = steps_per_launch * bytes_per_pdhg_iter(c) + ph.S_loc * solve_bytes_per_scenario(c)
+    gbs = pd_bytes / (pd_ms / 1000.0) / 1e9
+    n, m, nnz = farmer_dims(c)
+    return {"workload": f"farmer PH, {S} scenarios ({args.scens} per GPU), crops_multiplier={c} "
+                        f"(n={n}, m={m}, nnz={nnz} per scenario), rho={args.rho}",
+            "value": round(S * args.hbm_steps / dt, 2), "unit": "solves/s",
+            "ms_per_step": round(dt / args.hbm_steps * 1000.0, 3), "steps": args.hbm_steps,
+            "iter0_s": round(t_iter0, 3), "iter0_not_optimal": nonopt0,
+            "pdhg_steps_per_solve": round(st[4] / max(st[3], 1), 1), "pdhg_steps_max": st[5],
+            "roofline": {"bound": "hbm", "kernel": "pdhg_kernel", "achieved": round(gbs, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "kernel_ms": round(pd_ms, 3), "alg_bytes_per_launch": round(pd_bytes),
+                         "traffic": pmc_traffic("pdhg_kernel", ph.S_loc, c)[0],
+                         "note": "algorithmic = the HBM traffic a streaming PDHG would need "
+                                 "(SURVEY 8(d) B_it per scenario-step); this kernel keeps each "
+                                 "scenario on chip, so frac > 1 is possible"}}
+
+
 def main():
     # everything but the final JSON line goes to stderr
     real_stdout = sys.stdout
@@ -138,6 +197,9 @@ def run():
     ap.add_argument("--cpu-sample", type=int, default=500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hbm-crops", type=int, default=100,
+                    help="crops_multiplier of the HBM-bound companion config (F3); 0 = skip")
+    ap.add_argument("--hbm-steps", type=int, default=5)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -264,6 +326,12 @@ def run():
                     "trivial_bound": tb, "Eobj": eobj, "scenarios": args.tol_scens,
                     "n_gpus": world}
 
+    # companion HBM-bound config: farmer crops_multiplier
+    # 100, 10k scenarios per GPU -- the PDHG kernel's regime
+    f3 = None
+    if args.hbm_crops > 0:
+        f3 = hbm_config(args, world, farmer, PH, opts)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -316,6 +384,7 @@ def run():
             "cached_fraction": round(cached_frac, 4),
             "ph_to_tol": tol_info,
             "cpu_baseline": cpu,
+            "hbm_config": f3,
         }
     else:
         out = None
