@@ -130,3 +130,63 @@ def test_two_rank_gloo_hydro_matches_oracle():
         assert abs(conv - oc) < 1e-8 * abs(oc)
         assert abs(eobj - oe) < 1e-8 * abs(oe)
         assert abs(tb - ot) < 1e-8 * abs(ot)
+
+
+def test_wxbar_csv_round_trip_and_checks(tmp_path):
+    """utils/wxbarutils: the reference's csv formats, round trip of W and
+    xbar, missing-variable and dual-feasibility errors (wxbarutils.py:212-261)."""
+    from mpisppy_amd.utils import wxbarutils as wx
+    from mpisppy_amd.examples import farmer
+    names = [f"scen{i}" for i in range(3)]
+    ph, conv, eobj, tb = _run_ph(_opts(PHIterLimit=3), names, farmer.scenario_creator)
+    wfile = tmp_path / "w.csv"
+    xfile = tmp_path / "xbar.csv"
+    wx.write_W_to_file(ph, str(wfile))
+    wx.write_xbar_to_file(ph, str(xfile))
+    wx.write_W_to_file(ph, str(tmp_path / "wdir"), sep_files=True)
+    lines = wfile.read_text().strip().split("\n")
+    assert len(lines) == 3 * ph.K and lines[0].startswith("scen0,DevotedAcreage[")
+    W0 = ph.W.clone()
+    xb0 = ph.xbar.clone()
+    ph.W.zero_()
+    ph.xbar.zero_()
+    wx.set_W_from_file(str(wfile), ph, 0)
+    assert torch.equal(ph.W, W0)
+    ph.W.zero_()
+    wx.set_W_from_file(str(tmp_path / "wdir"), ph, 0, sep_files=True)
+    assert torch.equal(ph.W, W0)
+    wx.set_xbar_from_file(str(xfile), ph)
+    assert torch.allclose(ph.xbar, xb0, rtol=0, atol=0)
+    assert torch.allclose(ph.xsqbar, xb0 * xb0)
+    # comments are ignored; a non-zero sum_s p_s W_s is rejected
+    bad = tmp_path / "bad.csv"
+    txt = "# comment\n" + "\n".join(lines[:-1]) + "\n" + lines[-1].rsplit(",", 1)[0] + ",12345.0\n"
+    bad.write_text(txt)
+    with pytest.raises(RuntimeError, match="dual feasibility"):
+        wx.set_W_from_file(str(bad), ph, 0)
+    miss = tmp_path / "miss.csv"
+    miss.write_text("\n".join(lines[:-1]) + "\n")
+    with pytest.raises(RuntimeError, match="missing"):
+        wx.set_W_from_file(str(miss), ph, 0)
+
+
+def test_wxbar_writer_reader_extensions(tmp_path):
+    """WXBarWriter writes after PH; WXBarReader loads the files before Iter0
+    of a new PH (wxbarwriter.py / wxbarreader.py)."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.utils.wxbarwriter import WXBarWriter
+    from mpisppy_amd.utils.wxbarreader import WXBarReader
+    from mpisppy_amd.examples import farmer
+    from cpu_batch import CPUBatch
+    names = [f"scen{i}" for i in range(3)]
+    wf, xf = str(tmp_path / "w.csv"), str(tmp_path / "x.csv")
+    ph = PH(_opts(PHIterLimit=3, W_fname=wf, Xbar_fname=xf), names, farmer.scenario_creator,
+            PH_extensions=WXBarWriter)
+    ph.batch = CPUBatch(ph.batch_data)
+    ph.ph_main()
+    ph2 = PH(_opts(PHIterLimit=3, init_W_fname=wf, init_Xbar_fname=xf), names,
+             farmer.scenario_creator, PH_extensions=WXBarReader)
+    ph2.batch = CPUBatch(ph2.batch_data)
+    ph2.PH_Prep()
+    assert torch.equal(ph2.W, ph.W)
+    assert torch.equal(ph2.xbar, ph.xbar)
