@@ -92,6 +92,15 @@ int ph_batch_bind(ph_batch_t b, const double *vals /*dev [nnz][S]*/,
  * nonant_col[k] is the column of nonant slot k, in the reference's
  * nonant order (scenario_tree.py:10-38, spbase.py:272-280).
  */
+/*
+ * Replace the column bounds of every scenario (dev [n][S] each, copied):
+ * nonants fixed at a candidate xhat (l = u) for the inner-bound solves of
+ * extensions/xhatbase.py:_try_one (_fix_nonants / _restore_nonants), and
+ * back.  The scaling is unchanged (it depends on the matrix only); the
+ * active-set cache is invalidated.
+ */
+int ph_batch_set_bounds(ph_batch_t b, const double *l, const double *u);
+
 int ph_batch_set_nonants(ph_batch_t b, int32_t K,
                          const int32_t *nonant_col /*host [K]*/);
 

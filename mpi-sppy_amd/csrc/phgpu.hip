@@ -2359,6 +2359,22 @@ int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const doubl
   return PH_OK;
 }
 
+int ph_batch_set_bounds(ph_batch_t b, const double *l, const double *u) {
+  if (!b || !b->bound || !l || !u) return fail(PH_EINVAL, "ph_batch_set_bounds: bad arguments");
+  const size_t Sn = (size_t)b->S * b->n;
+  HIP_OK(hipMemcpyAsync(b->d_l, l, Sn * 8, hipMemcpyDeviceToDevice, b->stream));
+  HIP_OK(hipMemcpyAsync(b->d_u, u, Sn * 8, hipMemcpyDeviceToDevice, b->stream));
+  if (b->d_sb) {
+    hipLaunchKernelGGL(static_block_kernel, dim3((b->S + 3) / 4), dim3(256), 0, b->stream, b->S,
+                       b->n, b->m, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_dc, b->d_dr,
+                       b->d_sb);
+    HIP_OK(hipGetLastError());
+  }
+  // the cached active-set maps belong to the old bounds
+  if (b->d_cache_ok) HIP_OK(hipMemsetAsync(b->d_cache_ok, 0, sizeof(int32_t) * b->S, b->stream));
+  return PH_OK;
+}
+
 int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
   if (!b || K < 0 || (K && !nonant_col)) return fail(PH_EINVAL, "ph_batch_set_nonants: bad arguments");
   std::vector<int32_t> slot(b->n, -1);

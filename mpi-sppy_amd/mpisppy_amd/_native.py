@@ -38,6 +38,7 @@ SIGNATURES = [
     ("ph_batch_set_stream", _c_int, [_c_ptr, _c_ptr]),
     ("ph_batch_bind", _c_int, [_c_ptr] + [_c_ptr] * 6),
     ("ph_batch_set_nonants", _c_int, [_c_ptr, _c_int, _c_ptr]),
+    ("ph_batch_set_bounds", _c_int, [_c_ptr, _c_ptr, _c_ptr]),
     ("ph_pdhg_solve", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_dbl, _c_dbl,
                                _c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_ptr,
                                ctypes.POINTER(SolveOpts)]),

@@ -243,6 +243,11 @@ class DeviceBatch:
             self.handle, self._summary.ctypes.data_as(_native._c_ptr)), "ph_batch_solve_summary")
         return tuple(int(v) for v in self._summary)
 
+    def set_bounds(self, l, u):
+        """Column bounds of every scenario ([n][S] device tensors, copied)."""
+        _native.check(self.lib.ph_batch_set_bounds(self.handle, _native.ptr(l), _native.ptr(u)),
+                      "ph_batch_set_bounds")
+
     def set_stream(self, stream_handle):
         """Point the library's launches at another HIP stream (a raw handle)."""
         _native.check(self.lib.ph_batch_set_stream(self.handle, ctypes.c_void_p(stream_handle)),

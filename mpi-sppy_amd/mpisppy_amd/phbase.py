@@ -340,6 +340,40 @@ class PHBase(SPBase):
         return self.comm.allreduce_host(
             [float(np.sum(self.local_prob[~self.scenario_feasible]))])[0]
 
+    # ------------------------------------------- fixed-nonant solves --
+    def _save_nonants(self):
+        """phbase.py _save_nonants: the current nonant values of every local
+        scenario (device copy)."""
+        cols = torch.as_tensor(self.batch_data.nonant_cols.astype(np.int64), device=self.device)
+        self._saved_nonant_cols = cols
+        self._saved_nonants = self.batch.x.view(self.batch.n, self.S_loc).index_select(0, cols).clone()
+
+    def _fix_nonants(self, xhat_slots):
+        """phbase.py _fix_nonants: every local scenario's nonants fixed at the
+        node-slot values xhat_slots [G] (l = u on the nonant columns)."""
+        b = self.batch
+        n, S = b.n, self.S_loc
+        vals = torch.as_tensor(np.asarray(xhat_slots, dtype=np.float64)[self.gid_host],
+                               device=self.device)               # [K][S]
+        cols = torch.as_tensor(self.batch_data.nonant_cols.astype(np.int64), device=self.device)
+        l = b.l.clone().view(n, S)
+        u = b.u.clone().view(n, S)
+        l[cols] = vals
+        u[cols] = vals
+        b.set_bounds(l.reshape(-1), u.reshape(-1))
+        x = b.x.view(n, S)
+        x[cols] = vals   # the warm start sits on the fixed values
+
+    def _unfix_nonants(self):
+        self.batch.set_bounds(self.batch.l, self.batch.u)
+
+    def _restore_nonants(self):
+        """phbase.py _restore_nonants: saved nonant values back, bounds freed."""
+        self._unfix_nonants()
+        if getattr(self, "_saved_nonants", None) is not None:
+            x = self.batch.x.view(self.batch.n, self.S_loc)
+            x[self._saved_nonant_cols] = self._saved_nonants
+
     # ---------------------------------------------------------- W I/O --
     def W_from_flat_list(self, flat_list):
         """phbase.py:601-617: flat list in (scenario, nonant) order."""

@@ -194,3 +194,26 @@ class OraclePH:
             self.W = [np.array(w, dtype=np.float64) for w in W]
         self.solve_loop(1.0, 0.0)
         return self.Ebound()
+
+
+def xhat_objective(scens, xhat_by_node, prob=None):
+    """extensions/xhatbase.py:_try_one restated: every scenario's nonants at
+    node nd fixed at xhat_by_node[nd] (in the node's nonant order), the
+    scenario LPs solved exactly (W and prox off), the expected objective in
+    the reference's sense; None if a scenario is infeasible."""
+    S = len(scens)
+    prob = np.array([s.prob if s.prob is not None else 1.0 / S for s in scens]) if prob is None \
+        else np.asarray(prob)
+    tot = []
+    for p, sc in zip(prob, scens):
+        l, u = sc.l.copy(), sc.u.copy()
+        for (nm, cp, idx) in sc.nodes:
+            v = np.asarray(xhat_by_node[nm], dtype=np.float64)
+            l[idx] = v
+            u[idx] = v
+        sgn = 1.0 if sc.sense == "min" else -1.0
+        x, y, feas = solve_scenario(sgn * sc.c, None, sc.A, sc.rl, sc.ru, l, u)
+        if not feas:
+            return None
+        tot.append(p * (float(sc.c @ x) + sc.const))
+    return math.fsum(tot)

@@ -94,8 +94,22 @@ class CPUBatch:
                 self.xbar_accum(*self._xa)
             self._advance()
 
+    _lu = None
+
+    def set_bounds(self, l, u):
+        self._lu = (l.view(self.n, self.S).numpy().copy(), u.view(self.n, self.S).numpy().copy())
+
+    @property
+    def l(self):
+        return torch.as_tensor(self.data.l.reshape(-1).copy())
+
+    @property
+    def u(self):
+        return torch.as_tensor(self.data.u.reshape(-1).copy())
+
     def _solve(self, W, rho, xbar, w_on, prox_on):
         d = self.data
+        L, U = (d.l, d.u) if self._lu is None else self._lu
         Wv = W.view(self.K, self.S).numpy(); rv = rho.view(self.K, self.S).numpy()
         xb = xbar.view(self.K, self.S).numpy()
         X = self.x.view(self.n, self.S)
@@ -104,7 +118,7 @@ class CPUBatch:
             g[d.nonant_cols] += w_on * Wv[:, s] - prox_on * rv[:, s] * xb[:, s]
             q[d.nonant_cols] += prox_on * rv[:, s]
             cst = prox_on * float(np.sum(rv[:, s] / 2 * xb[:, s] ** 2))
-            x, y, feas = solve_scenario(g, q, self._A(s), d.rl[:, s], d.ru[:, s], d.l[:, s], d.u[:, s])
+            x, y, feas = solve_scenario(g, q, self._A(s), d.rl[:, s], d.ru[:, s], L[:, s], U[:, s])
             X[:, s] = torch.as_tensor(x)
             v = 0.5 * float(q @ (x * x)) + float(g @ x) + cst
             self.pobj[s] = v

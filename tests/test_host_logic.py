@@ -190,3 +190,27 @@ def test_wxbar_writer_reader_extensions(tmp_path):
     ph2.PH_Prep()
     assert torch.equal(ph2.W, ph.W)
     assert torch.equal(ph2.xbar, ph.xbar)
+
+
+def test_xhat_try_one_matches_oracle():
+    """extensions/xhatbase._try_one on the host flow (CPU stand-in batch):
+    nonants of one scenario fixed in all, LPs solved, Eobjective == the
+    oracle's restatement; nonants and bounds restored afterwards."""
+    from mpisppy_amd.extensions.xhatbase import XhatBase, xhat_shuffle_inner_bound
+    from mpisppy_amd.examples import farmer
+    from oracle.ph_oracle import xhat_objective
+    names = [f"scen{i}" for i in range(3)]
+    ph, conv, eobj, tb = _run_ph(_opts(PHIterLimit=3), names, farmer.scenario_creator)
+    x_before = ph.batch.x.clone()
+    xb = XhatBase(ph)
+    obj = xb._try_one({"ROOT": "scen1"})
+    xn = x_before.view(ph.batch.n, 3)[list(ph.batch_data.nonant_cols), 1].numpy()
+    ref = xhat_objective([om.farmer(nm) for nm in names], {"ROOT": xn})
+    assert abs(obj - ref) <= 1e-9 * abs(ref)
+    cols = list(ph.batch_data.nonant_cols)
+    assert torch.equal(ph.batch.x.view(ph.batch.n, 3)[cols], x_before.view(ph.batch.n, 3)[cols])
+    assert ph.batch._lu is not None and np.array_equal(ph.batch._lu[0], ph.batch_data.l)
+    best, who = xhat_shuffle_inner_bound(ph, tries=3)
+    from oracle.ef import solve_ef
+    ef, _ = solve_ef([om.farmer(nm) for nm in names])
+    assert best >= ef - 1e-6 * abs(ef) and who in names
