@@ -3,14 +3,17 @@
 
 The spoke's per-W work -- ``solve_loop`` with W on and no prox, then
 ``Ebound`` with a serial-number check (``lagrangian_bounder.py:19-53``) -- runs
-as one batched LP launch on the same kernels as the PH hub.  The hub->spoke
-W transport (MPI RMA windows in the reference, ``spoke.py:59-99``) is outside
-this round's scope; ``localWs`` / ``serial_number`` are set by the caller.
+as one batched LP launch on the same kernels as the PH hub.  W reaches the
+spoke either as flat lists (``main(W_stream)``, ``localWs``) or, inside the
+in-process wheel (``cylinders/hub.py``), as a device-to-device copy of the
+hub's W tensor (``hub_sync``) in place of the reference's RMA windows
+(``spoke.py:59-99``).
 """
 
 
 class LagrangianOuterBound:
     converger_spoke_char = "L"
+    bound_kind = "outer"
 
     def __init__(self, opt, cylinder_size=1):
         self.opt = opt
@@ -63,6 +66,22 @@ class LagrangianOuterBound:
             if b is not None:
                 self.bound = b
         return self.bound
+
+    # ---- in-process wheel (cylinders/hub.py)
+    def spoke_init(self):
+        self.lagrangian_prep()
+        self.trivial_bound = self.lagrangian()
+        self.bound = self.trivial_bound
+
+    def hub_sync(self, hub_opt):
+        """The hub's current W (device copy, same local scenarios), then a bound."""
+        self.opt.W.copy_(hub_opt.W)
+        self.serial_number += 1
+        b = self.lagrangian()
+        if b is not None and (self.bound is None or
+                              (b > self.bound if self.opt.is_minimizing else b < self.bound)):
+            self.bound = b
+        return b
 
     def finalize(self):
         self.final_bound = self._set_weights_and_solve()

@@ -470,7 +470,8 @@ class PHBase(SPBase):
         converger, hub/spoke communicator or per-iteration printing)."""
         o = self.PHoptions
         return (o.get("device_loop", True) and self.PH_extensions is None
-                and self.PH_converger is None and self.spcomm is None
+                and self.PH_converger is None
+                and (self.spcomm is None or hasattr(self.spcomm, "sync_every"))
                 and not o["display_progress"] and not o["display_convergence_detail"]
                 and not o.get("display_timing", False))
 
@@ -504,8 +505,11 @@ class PHBase(SPBase):
         b = self.batch
         chunk = int(chunk or self.PHoptions.get("device_loop_chunk", 16))
         if self.conv_hist is None or self.conv_hist.numel() < max(iter_limit, 1):
-            self.conv_hist = torch.zeros(max(iter_limit, 1024), dtype=torch.float64,
-                                         device=self.device)
+            old = self.conv_hist
+            size = max(iter_limit, 1024, 0 if old is None else 2 * old.numel())
+            self.conv_hist = torch.zeros(size, dtype=torch.float64, device=self.device)
+            if old is not None:
+                self.conv_hist[:old.numel()] = old
             self._loop_graphs = {}  # captured pointers changed
         b.loop_reset(start_iter, iter_limit, convthresh)
         b.loop_enable(True)
@@ -576,7 +580,24 @@ class PHBase(SPBase):
         """phbase.py:1472-1566: Xbar -> W -> conv -> [hub] -> break? -> solve."""
         if self._device_loop_ok():
             max_iterations = int(self.PHoptions["PHIterLimit"])
-            stop, it = self.run_device_loop(0, max_iterations, float(self.PHoptions["convthresh"]))
+            thresh = float(self.PHoptions["convthresh"])
+            if self.spcomm is None:
+                stop, it = self.run_device_loop(0, max_iterations, thresh)
+            else:
+                # hub: device-loop chunks of sync_every iterations, the spokes
+                # synced and the gap tested between chunks (phbase.py:1517-1521)
+                every = int(self.spcomm.sync_every)
+                stop, it = 0, 0
+                while it < max_iterations:
+                    stop, it = self.run_device_loop(it, min(it + every, max_iterations), thresh,
+                                                    chunk=every)
+                    self._PHIter = it
+                    if stop == 1:
+                        break
+                    self.spcomm.sync()
+                    if self.spcomm.is_converged():
+                        global_toc("Cylinder convergence", self.cylinder_rank == 0)
+                        break
             self._PHIter = it
             hist = self.conv_hist[:it].cpu().numpy() if it > 0 else np.zeros(0)
             self.conv_history = [float(v) for v in hist]

@@ -49,3 +49,41 @@ def option_string_to_dict(ostr):
         else:
             out[tok] = None
     return out
+
+
+def spin_the_wheel(hub_dict, list_of_spoke_dict, comm_world=None):
+    """sputils.py:24-131, in process: every rank builds the hub's opt object
+    and every spoke's (each over the rank's own scenarios, each with its own
+    device batch), the spokes are attached to the hub, and the hub runs PH,
+    syncing the spokes every ``hub_kwargs["sync_every"]`` iterations.
+    Returns (hub, hub_dict) like the reference's (spcomm, opt_dict)."""
+    if "hub_class" not in hub_dict:
+        raise RuntimeError("The hub_dict must contain a 'hub_class' key specifying the hub class to use")
+    if "opt_class" not in hub_dict:
+        raise RuntimeError("The hub_dict must contain an 'opt_class' key specifying the SPBase "
+                           "class to use (e.g. PHBase, etc.)")
+    hub_dict.setdefault("hub_kwargs", {})
+    hub_dict.setdefault("opt_kwargs", {})
+    for sd in list_of_spoke_dict:
+        if "spoke_class" not in sd:
+            raise RuntimeError("Each spoke_dict must contain a 'spoke_class' key specifying the "
+                               "spoke class to use")
+        if "opt_class" not in sd:
+            raise RuntimeError("Each spoke_dict must contain an 'opt_class' key specifying the "
+                               "SPBase class to use (e.g. PHBase, etc.)")
+        sd.setdefault("spoke_kwargs", {})
+        sd.setdefault("opt_kwargs", {})
+    kw = dict(hub_dict["opt_kwargs"])
+    if comm_world is not None:
+        kw["mpicomm"] = comm_world
+    opt = hub_dict["opt_class"](**kw)
+    spokes = []
+    for sd in list_of_spoke_dict:
+        skw = dict(sd["opt_kwargs"])
+        if comm_world is not None:
+            skw["mpicomm"] = comm_world
+        spokes.append(sd["spoke_class"](sd["opt_class"](**skw), **sd["spoke_kwargs"]))
+    hub = hub_dict["hub_class"](opt, spokes, **hub_dict["hub_kwargs"])
+    hub.main()
+    hub.hub_finalize()
+    return hub, hub_dict

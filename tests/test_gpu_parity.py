@@ -195,3 +195,33 @@ def test_xhat_inner_bounds_match_oracle():
     assert (obj is None) == (ref is None), (obj, ref)
     if ref is not None:
         assert abs(obj - ref) / abs(ref) < 1e-7, (obj, ref)
+
+
+def test_spin_the_wheel_hub_lagrangian_xhat():
+    """utils.sputils.spin_the_wheel with the reference's dict structure
+    (examples/farmer/farmer_cylinders.py): PH hub + Lagrangian outer-bound
+    spoke + xhat shuffle inner-bound spoke on the GPU; the bounds bracket
+    the EF optimum and the hub stops on the relative gap."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.phbase import PHBase
+    from mpisppy_amd.cylinders.hub import PHHub
+    from mpisppy_amd.cylinders.lagrangian_bounder import LagrangianOuterBound
+    from mpisppy_amd.cylinders.xhatshufflelooper_bounder import XhatShuffleInnerBound
+    from mpisppy_amd.utils.sputils import spin_the_wheel
+    from mpisppy_amd.examples import farmer
+    from oracle.ef import solve_ef
+    names = [f"scen{i}" for i in range(30)]
+    base = dict(scenario_creator=farmer.scenario_creator, all_scenario_names=names)
+    hub_dict = {"hub_class": PHHub, "hub_kwargs": {"options": {"rel_gap": 0.002}, "sync_every": 5},
+                "opt_class": PH,
+                "opt_kwargs": dict(PHoptions=_opts(PHIterLimit=500, convthresh=-1.0), **base)}
+    spokes = [{"spoke_class": LagrangianOuterBound, "opt_class": PHBase,
+               "opt_kwargs": dict(PHoptions=_opts(PHIterLimit=500), **base)},
+              {"spoke_class": XhatShuffleInnerBound, "opt_class": PHBase,
+               "opt_kwargs": dict(PHoptions=_opts(PHIterLimit=500), **base)}]
+    hub, _ = spin_the_wheel(hub_dict, spokes)
+    ef, _ = solve_ef([om.farmer(nm) for nm in names])
+    assert hub.BestOuterBound <= ef * (1 - 1e-7)      # min: outer below, inner above
+    assert hub.BestInnerBound >= ef * (1 + 1e-7)
+    assert hub.compute_gap() <= 0.002
+    assert hub.opt._PHIter < 500

@@ -214,3 +214,34 @@ def test_xhat_try_one_matches_oracle():
     from oracle.ef import solve_ef
     ef, _ = solve_ef([om.farmer(nm) for nm in names])
     assert best >= ef - 1e-6 * abs(ef) and who in names
+
+
+def test_hub_with_lagrangian_and_xhat_spokes_closes_the_gap():
+    """cylinders/hub.PHHub with an in-process Lagrangian (outer) and xhat
+    shuffle (inner) spoke on farmer: valid bounds around the EF optimum and
+    termination on the relative gap (hub.py:119-137, 430-466)."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.phbase import PHBase
+    from mpisppy_amd.cylinders.hub import PHHub
+    from mpisppy_amd.cylinders.lagrangian_bounder import LagrangianOuterBound
+    from mpisppy_amd.cylinders.xhatshufflelooper_bounder import XhatShuffleInnerBound
+    from mpisppy_amd.examples import farmer
+    from cpu_batch import CPUBatch
+    from oracle.ef import solve_ef
+    names = [f"scen{i}" for i in range(3)]
+
+    def mk(cls, **kw):
+        o = cls(_opts(PHIterLimit=50, convthresh=-1.0, **kw), names, farmer.scenario_creator)
+        o.batch = CPUBatch(o.batch_data)
+        return o
+
+    hub_opt = mk(PH)
+    lag = LagrangianOuterBound(mk(PHBase))
+    xh = XhatShuffleInnerBound(mk(PHBase))
+    hub = PHHub(hub_opt, [lag, xh], options={"rel_gap": 0.01}, sync_every=2)
+    hub.main()
+    hub.hub_finalize()
+    ef, _ = solve_ef([om.farmer(nm) for nm in names])
+    assert hub.BestOuterBound <= ef + 1e-6 * abs(ef) <= hub.BestInnerBound + 2e-6 * abs(ef)
+    assert hub.compute_gap() <= 0.01
+    assert hub_opt._PHIter < 50
