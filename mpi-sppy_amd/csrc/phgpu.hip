@@ -1265,7 +1265,8 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     } else if (restart) {
       // PDLP primal weight update, smoothing 0.5
       const double dx = sqrt(v[6]), dy = sqrt(v[7]);
-      if (dx > 1e-12 && dy > 1e-12) omega = exp(0.5 * log(dy / dx) + 0.5 * log(omega));
+      // exp(0.5 log(dy/dx) + 0.5 log(omega)), without the FP64 exp/log
+      if (dx > 1e-12 && dy > 1e-12) omega = sqrt(dy / dx * omega);
     }
     if (restart) {
       set_steps();
