@@ -46,10 +46,34 @@ int fail(int code, const std::string &msg) {
 constexpr int WAVE = 64;
 constexpr int MAX_WAVES = 16;  // 1024-thread blocks
 
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v & 0xffffffffull), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xF, 0xF, false);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v & 0xffffffffull), l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __longlong_as_double((long long)readlane_u64((unsigned long long)__double_as_longlong(v), l));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  return __longlong_as_double((long long)dpp_u64<CTRL>((unsigned long long)__double_as_longlong(v)));
+}
+
+// Wave-wide sum, uniform result, without LDS: DPP within rows of 16 lanes
+// (xor 1, xor 2, half-mirror, mirror), then the four row sums by readlane
+// (fixed order: deterministic).  All 64 lanes must be active.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, WAVE);
-  return v;
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
 // A wave-uniform double moved to scalar registers (the compiler cannot
@@ -418,14 +442,15 @@ __device__ __forceinline__ void kkt_terms_col(double XN, double G, double Q, dou
                                               double DC, double aty, double &lam_s,
                                               double (&v)[NV]) {
   lam_s = Q * XN + G - aty;
-  const double lam = lam_s / DC;  // unscaled reduced cost
+  const double idc = 1.0 / DC;  // one division per column
+  const double lam = lam_s * idc;  // unscaled reduced cost
   const double xu = XN * DC;
   const double lu = L * DC, uu = U * DC;
   const double lp = isfinite(lu) ? fmax(lam, 0.0) : 0.0;
   const double lm = isfinite(uu) ? fmin(lam, 0.0) : 0.0;
   const double rd = lam - lp - lm;
-  const double qx = Q / (DC * DC);
-  const double gu = G / DC;
+  const double qx = Q * idc * idc;
+  const double gu = G * idc;
   v[1] += rd * rd;
   v[2] += 0.5 * qx * xu * xu + gu * xu;
   v[3] += -0.5 * qx * xu * xu + (lp > 0.0 ? lp * lu : 0.0) + (lm < 0.0 ? lm * uu : 0.0);
@@ -435,8 +460,9 @@ __device__ __forceinline__ void kkt_terms_col(double XN, double G, double Q, dou
 template <int NV>
 __device__ __forceinline__ void kkt_terms_row(double AXN, double YN, double RL, double RU,
                                               double DR, double (&v)[NV]) {
-  const double axu = AXN / DR;
-  const double rlu = RL / DR, ruu = RU / DR;
+  const double idr = 1.0 / DR;  // one division per row
+  const double axu = AXN * idr;
+  const double rlu = RL * idr, ruu = RU * idr;
   const double rp = axu - clampd(axu, rlu, ruu);
   const double yu = YN * DR;
   v[0] += rp * rp;
@@ -1590,20 +1616,6 @@ constexpr int RG_R0 = RG_W - 1 - RG_K; // first right-hand-side column = max unk
 // LDS staging: the KKT rows, later the 1+K product vectors (x and y parts)
 constexpr int RG_KST = (RG_R0 * RG_W > 2 * (1 + RG_K) * WAVE) ? RG_R0 * RG_W : 2 * (1 + RG_K) * WAVE;
 
-template <int CTRL>
-__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v & 0xffffffffull), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xF, 0xF, false);
-  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-}
-__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v & 0xffffffffull), l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
-  return ((unsigned long long)hi << 32) | lo;
-}
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  return __longlong_as_double((long long)readlane_u64((unsigned long long)__double_as_longlong(v), l));
-}
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) {
   return a > b ? a : b;
 }
