@@ -228,6 +228,18 @@ int ph_loop_conv_local(ph_batch_t b, const double *absdiff /*dev [S]*/,
                        const int32_t *seg /*dev [R+1]*/, int32_t R,
                        const double *cnt /*dev [R]*/, double nproc,
                        double *parts /*dev [R] out*/, double *conv_hist);
+/*
+ * One rank: ph_update_w and ph_loop_conv_local in one launch.  wconv[s] =
+ * 1 / (cnt of the reference rank holding scenario s) / nproc, so conv =
+ * sum_s absdiff[s] * wconv[s] (phbase.py:254-276); same outputs as the two
+ * calls (conv up to summation order), plus the stop test.
+ */
+int ph_loop_update_w_conv(ph_batch_t b, const double *x /*dev [n*S]*/,
+                          const double *sums /*dev [2G]*/, int32_t G,
+                          const int32_t *gid /*dev [K*S]*/, const double *rho,
+                          const double *w_coeff /*dev [K*S] or NULL*/, double *xbar,
+                          double *xsqbar, double *W, double *absdiff /*dev [S]*/,
+                          const double *wconv /*dev [S]*/, double *conv_hist);
 int ph_loop_status(ph_batch_t b, int64_t *out /*host [8]*/);
 
 /*

@@ -2027,6 +2027,40 @@ __global__ void __launch_bounds__(1024) segment_sum_kernel(
   if (threadIdx.x == 0) out[r] = acc[0];
 }
 
+// ------------------------------------------------------------------------
+// Multi-block reductions with a last-block combine: every block publishes
+// its partials, takes a ticket, and the block that takes the last ticket
+// sums the partials in block order (deterministic) and resets the ticket.
+// Partials and the ticket move only through agent-scope atomic loads and
+// stores (coherent across the XCDs' L2s): no release fence, which on gfx950
+// writes back the whole L2 and costs microseconds per block.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ void pub(double *p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double sub(const double *p) {
+  return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The publishing stores of thread 0 precede its ticket: they are complete
+// (vmcnt drained) before the ticket's atomic is issued.
+__device__ __forceinline__ bool last_block(int32_t *ticket) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  return last;
+}
+__device__ __forceinline__ void reset_ticket(int32_t *ticket) {
+  __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int POST_BLOCK = 256;
+constexpr int POST_COMB = 2048;  // LDS doubles of a combine chunk
+
 // Block 0: (not optimal, sum iters, max iters, polished, cached) of the last
 // solve (polished: how 1/2, cached: how 3).
 // A reduction instead of per-workgroup atomics on one address, which
@@ -2095,6 +2129,63 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
   }
 }
 
+// Single-rank device loop: Compute_Xbar's broadcast + Update_W (as
+// update_w_kernel) fused with convergence_diff: conv = sum_s absdiff_s * wc_s
+// (wc_s = 1 / (count of the reference rank holding s) / ref_n_proc, i.e.
+// phbase.py:254-276's per-rank means summed over ranks), into conv_hist, and
+// the stop test before the solve; the last block also clears the solve's
+// work-list counters.
+__global__ void __launch_bounds__(POST_BLOCK) update_w_conv_kernel(
+    int S, int K, const double *__restrict__ x, const int32_t *__restrict__ nonant_col,
+    const double *__restrict__ sums, int G, const int32_t *__restrict__ gid,
+    const double *__restrict__ rho, const double *__restrict__ wc,
+    double *__restrict__ xbar, double *__restrict__ xsqbar, double *__restrict__ W,
+    double *__restrict__ absdiff, const double *__restrict__ wconv, double *__restrict__ part,
+    int32_t *ticket, LoopCtl *ctl, double *__restrict__ hist, int32_t *ctr) {
+  __shared__ double red[MAX_WAVES];
+  if (stopped(ctl)) return;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  double acc = 0.0;
+  if (s < S) {
+    for (int k = 0; k < K; ++k) {
+      const size_t o = (size_t)k * S + s;
+      const int g = gid[o];
+      const double xb = sums[g], xsq = sums[G + g];
+      const double xv = x[(size_t)nonant_col[k] * S + s];
+      xbar[o] = xb;
+      xsqbar[o] = xsq;
+      const double d = xv - xb;
+      double w = W[o] + rho[o] * d;
+      if (wc) w *= wc[o];
+      W[o] = w;
+      acc += fabs(d);
+    }
+    absdiff[s] = acc;
+  }
+  double v[1] = {s < S ? acc * wconv[s] : 0.0};
+  block_sum<1>(v, red);
+  if (threadIdx.x == 0) pub(part + blockIdx.x, v[0]);
+  if (!last_block(ticket)) return;
+  __shared__ double comb[POST_COMB];
+  double conv = 0.0;  // (thread 0) partials in block order, staged a chunk at a time
+  for (int c0 = 0; c0 < (int)gridDim.x; c0 += POST_COMB) {
+    const int nc = min(POST_COMB, (int)gridDim.x - c0);
+    for (int b = threadIdx.x; b < nc; b += blockDim.x) comb[b] = sub(part + c0 + b);
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int b = 0; b < nc; ++b) conv += comb[b];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    hist[ctl->iter - 1] = conv;
+    if (conv < ctl->thresh) ctl->stop = 1;
+    ctr[0] = 0;
+    ctr[1] = 0;
+    ctr[2] = 0;
+    reset_ticket(ticket);
+  }
+}
+
 __global__ void __launch_bounds__(256) eval_obj_kernel(
     int S, int n, const double *__restrict__ c, const int32_t *__restrict__ slot_of_col,
     const double *__restrict__ x, const double *__restrict__ W,
@@ -2137,7 +2228,7 @@ struct ph_batch {
   int32_t *d_cache_ok = nullptr;
   unsigned long long *d_hint = nullptr;
   int32_t *d_hint_ok = nullptr, *d_wl = nullptr, *d_wl2 = nullptr;
-  int32_t *d_ctr = nullptr;  // [4]: miss list count, pdhg queue, pdhg list count
+  int32_t *d_ctr = nullptr;  // [6]: miss list count, pdhg queue, pdhg list count, post ticket, W/conv ticket
   double *d_sb = nullptr;    // [S][4n+3m] static block (polish-size scenarios)
   LoopCtl *d_ctl = nullptr;  // device loop control
   bool loop_on = false;
@@ -2148,6 +2239,8 @@ struct ph_batch {
   std::vector<hipEvent_t> ev;  // 4 per recorded solve: as0, as1 (=pd0), pd1, spare
   size_t ev_used = 0;
   int pdhg_grid = 0;         // resident blocks of the pdhg kernel (0: not yet known)
+  double *d_part = nullptr;  // partials of the multi-block reductions
+  size_t part_cap = 0;
   // extra chunks of lines longer than LINE_D (see LineRegs)
   int xr = 0, xc = 0;
   int32_t *d_r_pb = nullptr, *d_r_pos = nullptr, *d_r_len = nullptr;
@@ -2278,12 +2371,21 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
       (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
-      (rc = dalloc(&b->d_summary, 5)) || (rc = dalloc(&b->d_ctr, 4)) || (rc = dalloc(&b->d_ctl, 1)) ||
+      (rc = dalloc(&b->d_summary, 5)) || (rc = dalloc(&b->d_ctr, 6)) || (rc = dalloc(&b->d_ctl, 1)) ||
       (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
     ph_batch_destroy(b);
     return rc;
+  }
+  b->part_cap = (size_t)((S + POST_BLOCK - 1) / POST_BLOCK);
+  if (dalloc(&b->d_part, b->part_cap)) {
+    ph_batch_destroy(b);
+    return fail(PH_EHIP, "ph_batch_create: allocation failed");
+  }
+  if (hipMemsetAsync(b->d_ctr, 0, 6 * sizeof(int32_t), b->stream) != hipSuccess) {
+    ph_batch_destroy(b);
+    return fail(PH_EHIP, "ph_batch_create: clearing counters failed");
   }
   std::vector<int32_t> noslot(n, -1);
   auto cp = [&](void *d, const void *h, size_t bytes) {
@@ -2479,7 +2581,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     b->pdhg_grid = std::max(1, per_cu) * std::max(1, cus);
   }
   // (in the device loop the convergence kernel has cleared the counters)
-  if (!b->loop_on) HIP_OK(hipMemsetAsync(b->d_ctr, 0, 4 * sizeof(int32_t), b->stream));
+  if (!b->loop_on) HIP_OK(hipMemsetAsync(b->d_ctr, 0, 3 * sizeof(int32_t), b->stream));
   hipEvent_t *tev = nullptr;
   if (b->timing) {
     if (b->ev_used + 4 > b->ev.size()) {
@@ -2518,7 +2620,9 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     if (!(a.cache && a.warm)) HIP_OK(hipEventRecord(tev[1], b->stream));
     HIP_OK(hipEventRecord(tev[2], b->stream));
   }
-  const int grid = std::min(b->S, b->pdhg_grid);
+  // behind the cache and the polish the PDHG list is short (usually empty):
+  // a small grid drains it from the queue and costs little when empty
+  const int grid = std::min(b->S, (a.cache && a.warm) ? std::min(b->pdhg_grid, 64) : b->pdhg_grid);
   DISPATCH_GEOM(b->block, b->per, b->ext, {
     hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(grid), dim3(B_), lds, b->stream, a);
   });
@@ -2639,6 +2743,24 @@ int ph_loop_conv(ph_batch_t b, const double *parts, const double *cnt, int32_t R
   return PH_OK;
 }
 
+int ph_loop_update_w_conv(ph_batch_t b, const double *x, const double *sums, int32_t G,
+                          const int32_t *gid, const double *rho, const double *w_coeff,
+                          double *xbar, double *xsqbar, double *W, double *absdiff,
+                          const double *wconv, double *conv_hist) {
+  if (!b || !b->loop_on || !x || !sums || G <= 0 || !gid || !rho || !xbar || !xsqbar || !W ||
+      !absdiff || !wconv || !conv_hist)
+    return fail(PH_EINVAL, "ph_loop_update_w_conv: bad arguments (or loop not enabled)");
+  if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_loop_update_w_conv: no nonants declared");
+  const int nb = (b->S + POST_BLOCK - 1) / POST_BLOCK;
+  if ((size_t)nb > b->part_cap)
+    return fail(PH_EINVAL, "ph_loop_update_w_conv: reduction buffer too small");
+  hipLaunchKernelGGL(update_w_conv_kernel, dim3(nb), dim3(POST_BLOCK), 0, b->stream, b->S, b->K, x,
+                     b->d_nonant_col, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
+                     b->d_part, b->d_ctr + 4, b->d_ctl, conv_hist, b->d_ctr);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
 int ph_loop_conv_local(ph_batch_t b, const double *absdiff, const int32_t *seg, int32_t R,
                        const double *cnt, double nproc, double *parts, double *conv_hist) {
   if (!b || !b->loop_on || !absdiff || !seg || R <= 0 || !cnt || !parts || !conv_hist)
@@ -2726,7 +2848,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
-                  b->d_sb,
+                  b->d_sb, b->d_part,
                   b->d_ctl,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)

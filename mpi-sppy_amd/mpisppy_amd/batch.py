@@ -279,6 +279,14 @@ class DeviceBatch:
                                                   _native.ptr(parts), _native.ptr(conv_hist)),
                       "ph_loop_conv_local")
 
+    def loop_update_w_conv(self, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
+                           conv_hist):
+        _native.check(self.lib.ph_loop_update_w_conv(
+            self.handle, _native.ptr(self.x), _native.ptr(sums), G, _native.ptr(gid),
+            _native.ptr(rho), _native.ptr(w_coeff), _native.ptr(xbar), _native.ptr(xsqbar),
+            _native.ptr(W), _native.ptr(absdiff), _native.ptr(wconv), _native.ptr(conv_hist)),
+            "ph_loop_update_w_conv")
+
     def loop_conv(self, parts, cnt, nproc, conv_hist):
         _native.check(self.lib.ph_loop_conv(self.handle, _native.ptr(parts), _native.ptr(cnt),
                                             parts.numel(), float(nproc),

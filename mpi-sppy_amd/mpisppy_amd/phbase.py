@@ -110,6 +110,11 @@ class PHBase(SPBase):
         self.conv_cnt = np.array([max(len(sl), 1) * K for sl in slices], dtype=np.float64)
         self.conv_parts = torch.zeros(R, **f64)
         self.conv_cnt_dev = torch.as_tensor(self.conv_cnt, **f64)
+        # the same weights per local scenario, 1/cnt[r(s)]/R (fused W + conv)
+        wconv = np.zeros(S)
+        for r in range(R):
+            wconv[seg[r]:seg[r + 1]] = 1.0 / self.conv_cnt[r] / R
+        self.conv_w = torch.as_tensor(wconv, **f64)
         self.conv_hist = None
         self._loop_graphs = {}
         self.scenario_feasible = np.ones(S, dtype=bool)
@@ -483,13 +488,13 @@ class PHBase(SPBase):
         broadcast and Update_W are one kernel (update_w with W), which writes
         what the two reference calls write."""
         b = self.batch
-        self.comm.allreduce_(self.xsums)
-        b.update_w(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
-                   self.xsqbar, self.W, self.absdiff)
-        if self.comm.size == 1:
-            b.loop_conv_local(self.absdiff, self.conv_seg, self.conv_cnt_dev, self.ref_n_proc,
-                              self.conv_parts, self.conv_hist)
+        if self.comm.size == 1:  # one kernel: broadcast, Update_W, convergence_diff
+            b.loop_update_w_conv(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
+                                 self.xsqbar, self.W, self.absdiff, self.conv_w, self.conv_hist)
         else:
+            self.comm.allreduce_(self.xsums)
+            b.update_w(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
+                       self.xsqbar, self.W, self.absdiff)
             b.segment_sum(self.absdiff, None, self.conv_seg, self.conv_parts)
             self.comm.allreduce_(self.conv_parts)
             b.loop_conv(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc, self.conv_hist)

@@ -66,6 +66,17 @@ class CPUBatch:
         self.segment_sum(absdiff, None, seg, parts)
         self.loop_conv(parts, cnt, nproc, conv_hist)
 
+    def loop_update_w_conv(self, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
+                           conv_hist):
+        if self._stopped():
+            return
+        self.update_w(sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff)
+        c = self._ctl
+        v = float((absdiff * wconv).sum())
+        conv_hist[c["iter"] - 1] = v
+        if v < c["thresh"]:
+            c["stop"] = 1
+
     def loop_conv(self, parts, cnt, nproc, conv_hist):
         c = self._ctl
         if c["stop"]:
