@@ -56,16 +56,39 @@ def solve_bytes_per_scenario(c):
     return 8 * (nnz + (n + m) + 3 * n + 2 * m + 2 * (n + m) + 3 * K + 13)
 
 
-def cpu_baseline(c, sample_scens, min_seconds=10.0):
-    """Oracle subproblem engine (HiGHS 1.8 from scipy) timed on this host,
-    one core, on a bounded sample of the same workload: the prox-QPs of one
-    PH iteration (W and xbar from an oracle Iter0) for `sample_scens` farmer
-    scenarios, solved sequentially like the reference's solve_loop, repeated
-    until at least `min_seconds` of CPU work has been timed."""
+_CPU_PROBS = None  # the sample's subproblems, inherited by forked workers
+
+
+def _cpu_worker(arg):
+    """Solve the sample's subproblems w, w+k, w+2k, ... cyclically until
+    `min_seconds` have passed; (solves, seconds)."""
+    from oracle.solve import _highs_solve
+    w, k, min_seconds = arg
+    mine = _CPU_PROBS[w::k]
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        for pr in mine:
+            _highs_solve(*pr)
+        n += len(mine)
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds:
+            return n, dt
+
+
+def cpu_baseline(c, sample_scens, min_seconds=10.0, cores=16):
+    """Oracle subproblem engine (HiGHS 1.8 from scipy) timed on this host on a
+    bounded sample of the same workload: the prox-QPs of one PH iteration (W
+    and xbar from an oracle Iter0) for `sample_scens` farmer scenarios, solved
+    sequentially per process like the reference's solve_loop (one rank per
+    core), each process cycling its share for `min_seconds`.
+    Timed on 1 core and on `cores` forked processes.  Runs before anything
+    touches the GPU (the workers are forked)."""
+    global _CPU_PROBS
+    import multiprocessing as mp
     sys.path.insert(0, ROOT)
     from oracle import models as om
     from oracle.ph_oracle import OraclePH
-    from oracle.solve import _highs_solve
     names = [f"scen{i}" for i in range(sample_scens)]
     scens = [om.farmer(nm, c) for nm in names]
     ph = OraclePH({"PHIterLimit": 1, "defaultPHrho": 1.0, "convthresh": 0.0}, scens)
@@ -77,19 +100,23 @@ def cpu_baseline(c, sample_scens, min_seconds=10.0):
         g, q, _ = ph._terms(s, 1.0, 1.0)
         sc = scens[s]
         probs.append((g, q, sc.A, sc.rl, sc.ru, sc.l, sc.u))
-    n_solved = 0
-    t0 = time.perf_counter()
-    while True:
-        for pr in probs:
-            _highs_solve(*pr)
-        n_solved += len(probs)
-        dt = time.perf_counter() - t0
-        if dt >= min_seconds:
-            break
-    return {"value": round(n_solved / dt, 2), "unit": "solves/s", "cores": 1, "kind": "port",
-            "sample": f"{n_solved} solves ({len(probs)} distinct farmer c={c} PH prox-QP "
-                      f"subproblems of one PH iteration after Iter0, cycled), HiGHS 1.8.0 QP "
-                      f"via scipy, sequential on 1 core, {dt:.1f} s"}
+    _CPU_PROBS = probs
+    n1, dt1 = _cpu_worker((0, 1, min_seconds))
+    one = n1 / dt1
+    cores = max(1, min(cores, len(os.sched_getaffinity(0)), len(probs)))
+    value, dtm, nm = one, dt1, n1
+    if cores > 1:
+        with mp.get_context("fork").Pool(cores) as pool:
+            res = pool.map(_cpu_worker, [(w, cores, min_seconds) for w in range(cores)])
+        nm = sum(r[0] for r in res)
+        dtm = max(r[1] for r in res)
+        value = nm / dtm
+    return {"value": round(value, 2), "unit": "solves/s", "cores": cores, "kind": "port",
+            "value_1core": round(one, 2),
+            "sample": f"{len(probs)} distinct farmer c={c} PH prox-QP subproblems of one PH "
+                      f"iteration after Iter0, cycled; HiGHS 1.8.0 QP via scipy; {cores} "
+                      f"processes x {dtm:.1f} s ({nm} solves), and 1 process x {dt1:.1f} s "
+                      f"({n1} solves)"}
 
 
 def pmc_traffic(kname, S_loc, c):
@@ -99,7 +126,7 @@ def pmc_traffic(kname, S_loc, c):
     FETCH_SIZE x2 correction applied there), when they were collected on
     this workload; else None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")),
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary*.json")),
                        reverse=True):
         try:
             with open(path) as f:
@@ -196,6 +223,8 @@ def run():
     ap.add_argument("--convthresh", type=float, default=1e-4)
     ap.add_argument("--cpu-sample", type=int, default=500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-cores", type=int, default=16,
+                    help="CPU-baseline processes (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hbm-crops", type=int, default=100,
                     help="crops_multiplier of the HBM-bound companion config (F3); 0 = skip")
@@ -205,6 +234,12 @@ def run():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None  # CPU baseline first: its worker processes fork before any GPU use
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args.crops, args.cpu_sample, args.cpu_seconds, args.cpu_cores)
+        except Exception as e:  # the baseline must not kill the GPU number
+            cpu = {"value": None, "error": repr(e)}
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
     if world > 1:
@@ -332,14 +367,8 @@ def run():
     if args.hbm_crops > 0:
         f3 = hbm_config(args, world, farmer, PH, opts)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            cpu = cpu_baseline(c, args.cpu_sample, args.cpu_seconds)
-            if tol_info is not None and cpu.get("value"):
-                cpu["ph_to_tol_projected_s"] = round(tol_info["ph_iterations"] * S / cpu["value"], 1)
-        except Exception as e:  # the baseline must not kill the GPU number
-            cpu = {"value": None, "error": repr(e)}
+    if cpu is not None and tol_info is not None and cpu.get("value"):
+        cpu["ph_to_tol_projected_s"] = round(tol_info["ph_iterations"] * S / cpu["value"], 1)
 
     if rank == 0:
         value = S * args.steps / dt

@@ -17,7 +17,7 @@ import os
 import sys
 
 KERNELS = ("active_set_kernel", "polish_kernel", "pdhg_kernel", "summary_kernel",
-           "update_w_kernel", "loop_conv_local_kernel")
+           "update_w_conv_kernel", "update_w_kernel", "loop_conv_local_kernel")
 
 
 def short(name):
