@@ -37,7 +37,9 @@ class LagrangianOuterBound:
     def lagrangian(self):
         """lagrangian_bounder.py:19-57: batched LP solves + Ebound (serial check)."""
         verbose = self.opt.options["verbose"]
-        self.opt.solve_loop(solver_options=self.opt.current_solver_options, dtiming=False,
+        self.opt.solve_loop(
+            solver_options=self.opt._bound_solver_options(self.opt.current_solver_options),
+            dtiming=False,
                             gripe=True, tee=False, verbose=verbose)
         serial_number = self.get_serial_number()
         bound, extra_sums = self.opt.Ebound(verbose, extra_sum_terms=[serial_number])

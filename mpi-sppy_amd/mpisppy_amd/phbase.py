@@ -145,6 +145,19 @@ class PHBase(SPBase):
                     warnings.warn(f"solver option {k}={v} ignored by the PDHG batch solver")
         return kw
 
+    def _bound_solver_options(self, solver_options):
+        """Solver options for the bound solves (post_solve_bound, the
+        Lagrangian spoke).  The per-scenario bound is the dual objective of
+        the returned (x, y); a dual residual on a one-sided column makes it
+        exact only up to that residual times |x|, so at the 1e-9 default the
+        10k-scenario farmer bound overshot the EF optimum by 3e-8 relative.
+        Unless the caller sets ``pdhg_tol``, bound solves run at
+        PHoptions["bound_pdhg_tol"] (default 1e-12), which the exact
+        active-set polish reaches in FP64."""
+        o = dict(solver_options or {})
+        o.setdefault("pdhg_tol", self.PHoptions.get("bound_pdhg_tol", 1e-12))
+        return o
+
     # ------------------------------------------------- W / prox attach --
     def attach_xbars(self):
         """phbase.py:1622-1632."""
@@ -689,7 +702,8 @@ class PHBase(SPBase):
         if self.W_disabled:
             self._reenable_W()
         self._disable_prox()
-        self.solve_loop(solver_options=solver_options, dis_prox=False, gripe=True,
+        self.solve_loop(solver_options=self._bound_solver_options(solver_options),
+                        dis_prox=False, gripe=True,
                         tee=False, verbose=verbose)
         bound = self.Ebound(verbose)
         self._reenable_prox()

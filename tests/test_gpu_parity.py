@@ -225,3 +225,39 @@ def test_spin_the_wheel_hub_lagrangian_xhat():
     assert hub.BestInnerBound >= ef * (1 + 1e-7)
     assert hub.compute_gap() <= 0.002
     assert hub.opt._PHIter < 500
+
+
+def test_farmer_10k_ph_converges_to_extensive_form():
+    """BASELINE config F2 at full size (10,000 scenarios, c=1): the farmer
+    subproblems are LPs, so the PH fixed point is the EF optimum.  Checked
+    against tests/golden/farmer_ef.json (oracle EF, HiGHS simplex): xbar, the
+    PH objective (phbase.py:279-312), and the bounds of phbase.py:1454 and
+    :753-801 bracketing the EF value."""
+    import json
+    import os
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    with open(os.path.join(os.path.dirname(__file__), "golden", "farmer_ef.json")) as f:
+        gold = [g for g in json.load(f)["cases"] if g["S"] == 10000][0]
+    S = gold["S"]
+    names = [f"scen{i}" for i in range(S)]
+    opts = _opts(PHIterLimit=60000, defaultPHrho=1.0, convthresh=1e-6)
+    ph = PH(dict(opts), names, farmer.scenario_creator,
+            scenario_creator_kwargs={"crops_multiplier": 1})
+    conv, eobj, tb = ph.ph_main()
+    xbar = ph.xbar.view(ph.K, ph.S_loc)[:, 0].cpu().numpy()
+    ef, xef = gold["ef_obj"], np.array(gold["nonants"])
+    print(f"10k PH: iters {ph._PHIter} conv {conv:.3e} Eobj {eobj:.9f} EF {ef:.9f} "
+          f"trivial {tb:.6f} xbar {xbar} EF x {xef} rel {_rel(xbar, xef):.3e}")
+    assert conv < 1e-6
+    assert tb <= ef + 1e-9 * abs(ef)                      # minimization: a lower bound
+    assert abs(eobj - ef) / abs(ef) < 1e-6
+    assert _rel(xbar, xef) < 2e-5
+    # the bound's LP solves at the default 1e-9 relative KKT: the dual
+    # objective is exact only up to the dual residual on one-sided columns
+    lb9 = ph.post_solve_bound(solver_options={"pdhg_tol": 1e-9})
+    lb12 = ph.post_solve_bound()  # bound solves default to 1e-12
+    print(f"post_solve_bound tol 1e-9 {lb9:.6f} tol 1e-12 {lb12:.6f} EF {ef:.6f}")
+    assert abs(lb9 - ef) / abs(ef) < 1e-6
+    assert tb <= lb12 <= ef + 1e-12 * abs(ef)
+    assert (ef - lb12) / abs(ef) < 1e-6

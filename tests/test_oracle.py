@@ -107,3 +107,19 @@ def test_sslp_lp_relaxation_bounds():
     assert abs(ef_val - (-280.4902709111119)) < 1e-6
     assert abs(tb - (-291.989987012987)) < 1e-6
     assert orc.iters == 10 and 0.0 < conv < 0.05
+
+
+def test_farmer_ef_golden_fixture_reproduces():
+    # tests/golden/farmer_ef.json was written by tests/golden/make_golden.py;
+    # the S=1000 case is re-solved here (the 10k case takes ~15 s)
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "farmer_ef.json")) as f:
+        gold = [g for g in json.load(f)["cases"] if g["S"] == 1000][0]
+    scens = [om.farmer(f"scen{i}", 1, num_scens=1000) for i in range(1000)]
+    obj, xs = solve_ef(scens)
+    assert abs(obj - gold["ef_obj"]) <= 1e-9 * abs(obj)
+    idx = scens[0].nodes[0][2]
+    assert np.allclose([xs[0][i] for i in idx], gold["nonants"], rtol=1e-8)
+    # every scenario shares the first stage (non-anticipativity rows)
+    assert max(np.max(np.abs(x[idx] - xs[0][idx])) for x in xs) < 1e-7
