@@ -261,3 +261,55 @@ def test_farmer_10k_ph_converges_to_extensive_form():
     assert abs(lb9 - ef) / abs(ef) < 1e-6
     assert tb <= lb12 <= ef + 1e-12 * abs(ef)
     assert (ef - lb12) / abs(ef) < 1e-6
+
+
+@pytest.mark.parametrize("S,R", [(1, 1), (67, 3)])
+def test_farmer_ragged_sizes_and_reference_rank_count(S, R):
+    """Edge sizes: one scenario (xbar = x, W = 0, conv = 0 after one pass) and
+    a count that fills no whole wave/block (67 = 4*16 + 3), with the
+    convergence metric emulating a reference run on R MPI ranks
+    (phbase.py:254-276, rank slices sputils.py:625-628)."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    names = [f"scen{i}" for i in range(S)]
+    opts = _opts(PHIterLimit=25, defaultPHrho=1.0, convthresh=1e-4)
+    ph = PH(dict(opts, ref_n_proc=R), names, farmer.scenario_creator)
+    conv, eobj, tb = ph.ph_main()
+    orc = OraclePH(dict(opts), [om.farmer(n) for n in names], n_proc=R)
+    oc, oe, ot = orc.ph_main()
+    assert ph._PHIter == orc.iters
+    assert abs(tb - ot) / abs(ot) < 1e-6
+    assert abs(eobj - oe) / abs(oe) < 1e-5
+    xbar = ph.xbar.view(ph.K, ph.S_loc)[:, 0].cpu().numpy()
+    assert _rel(xbar, orc.xbar[0]) < 1e-5
+    W = ph.W.view(ph.K, ph.S_loc).cpu().numpy().T
+    assert _rel(W, np.array(orc.W)) < 1e-5
+    if S == 1:
+        assert conv == 0.0 and np.all(W == 0.0)
+    else:
+        assert abs(conv - oc) / abs(oc) < 1e-3
+
+
+def test_host_loop_device_loop_and_graphs_agree():
+    """The three ways of running iterk_loop (host loop with one solve_loop per
+    iteration, device loop with eager launches, device loop replayed as HIP
+    graphs) compute the same PH trajectory on farmer S=1000."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    names = [f"scen{i}" for i in range(1000)]
+    res = []
+    for mode in ({"device_loop": False}, {"device_loop": True, "device_loop_graphs": False},
+                 {"device_loop": True, "device_loop_graphs": True}):
+        opts = _opts(PHIterLimit=60, defaultPHrho=1.0, convthresh=1e-9, **mode)
+        ph = PH(dict(opts), names, farmer.scenario_creator)
+        conv, eobj, tb = ph.ph_main()
+        res.append((ph._PHIter, conv, eobj, tb, ph.xbar.cpu().numpy().copy(),
+                    ph.W.cpu().numpy().copy()))
+    it0, c0, e0, t0, x0, w0 = res[0]
+    for it, c, e, t, x, w in res[1:]:
+        assert it == it0 == 60
+        assert abs(c - c0) <= 1e-9 * abs(c0)
+        assert abs(e - e0) <= 1e-11 * abs(e0)
+        assert abs(t - t0) <= 1e-9 * abs(t0)  # Iter0 LP dual objectives at 1e-9 KKT
+        assert _rel(x, x0) < 1e-11
+        assert _rel(w, w0) < 1e-9
