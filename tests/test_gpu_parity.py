@@ -313,3 +313,63 @@ def test_host_loop_device_loop_and_graphs_agree():
         assert abs(t - t0) <= 1e-9 * abs(t0)  # Iter0 LP dual objectives at 1e-9 KKT
         assert _rel(x, x0) < 1e-11
         assert _rel(w, w0) < 1e-9
+
+
+def _gpu_rank_worker(rank, world, port, q):
+    """One PH rank on cuda:0 (both ranks share the box's single GPU; the
+    collectives go over gloo with host staging, the kernels are the N>1
+    device-loop path: update_w, segment_sum, loop_conv between allreduces)."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "mpi-sppy_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from mpisppy_amd.opt.ph import PH
+        from mpisppy_amd.examples import farmer
+        names = [f"scen{i}" for i in range(30)]
+        opts = _opts(PHIterLimit=40, defaultPHrho=1.0, convthresh=1e-4)
+        ph = PH(dict(opts), names, farmer.scenario_creator)
+        conv, eobj, tb = ph.ph_main()
+        xbar = ph.xbar.view(ph.K, ph.S_loc)[:, 0].cpu().numpy().tolist()
+        q.put((rank, conv, eobj, tb, ph._PHIter, xbar, list(ph.local_scenario_names)))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_two_ranks_on_gpu_match_oracle():
+    """The multi-rank device path on the GPU: farmer S=30 split 15/15 over two
+    ranks (sputils.py:625-628), xbar sums and conv partials allreduced every
+    iteration; iterations, conv, Eobj, trivial bound and xbar vs the oracle
+    run on 2 reference ranks."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][6] == [f"scen{i}" for i in range(15)]
+    assert res[1][6] == [f"scen{i}" for i in range(15, 30)]
+    opts = _opts(PHIterLimit=40, defaultPHrho=1.0, convthresh=1e-4)
+    orc = OraclePH(dict(opts), [om.farmer(f"scen{i}") for i in range(30)], n_proc=2)
+    oc, oe, ot = orc.ph_main()
+    for rank, conv, eobj, tb, iters, xbar, _ in res:
+        assert iters == orc.iters
+        assert abs(conv - oc) / abs(oc) < 1e-3
+        assert abs(eobj - oe) / abs(oe) < 1e-5
+        assert abs(tb - ot) / abs(ot) < 1e-6
+        assert _rel(xbar, orc.xbar[0]) < 1e-5
