@@ -240,6 +240,25 @@ int ph_loop_update_w_conv(ph_batch_t b, const double *x /*dev [n*S]*/,
                           const double *w_coeff /*dev [K*S] or NULL*/, double *xbar,
                           double *xsqbar, double *W, double *absdiff /*dev [S]*/,
                           const double *wconv /*dev [S]*/, double *conv_hist);
+/*
+ * Several ranks, one collective per iteration (what PHBase uses): the conv
+ * partials of a pass travel in the NEXT pass's Compute_Xbar allreduce (one
+ * buffer [2G | R]), so each pass runs
+ *   [allreduce sums|parts] ph_loop_conv_lagged  ph_update_w  ph_segment_sum
+ *   ph_loop_backup  ph_pdhg_solve
+ * ph_loop_conv_lagged tests the pending pass's conv (conv_hist[k-1]); when
+ * it is below convthresh it sets stop (1) and iter back to k, and the host
+ * restores x/y from the copies ph_loop_backup saved before pass k's solve --
+ * the reference's state at its break (phbase.py:1498-1553).  After the loop
+ * ends at the limit (stop 2) the host flushes the last pass's partials with
+ * one more allreduce + ph_loop_conv_lagged.  ph_loop_backup copies
+ * x[0..nx) -> x_save, y[0..ny) -> y_save and marks the current pass pending.
+ */
+int ph_loop_conv_lagged(ph_batch_t b, const double *parts /*dev [R]*/,
+                        const double *cnt /*dev [R]*/, int32_t R, double nproc,
+                        double *conv_hist /*dev [iter_limit]*/);
+int ph_loop_backup(ph_batch_t b, const double *x, double *x_save, int64_t nx,
+                   const double *y, double *y_save, int64_t ny);
 int ph_loop_status(ph_batch_t b, int64_t *out /*host [8]*/);
 
 /*

@@ -284,7 +284,7 @@ struct LoopCtl {
   int32_t stop;   // 0 running, 1 converged, 2 iteration limit
   int32_t iter;   // PH iteration of the current pass (1-based)
   int32_t limit;  // PHIterLimit
-  int32_t pad;
+  int32_t pend;   // lagged conv (several ranks): iteration whose partials wait, or 0
   double thresh;  // convthresh
   unsigned long long acc[6];  // not optimal, solves, iters sum, iters max, polished, cached
 };
@@ -1562,6 +1562,49 @@ __global__ void loop_conv_kernel(LoopCtl *c, const double *__restrict__ parts,
   ctr[2] = 0;
 }
 
+// Several ranks, one collective per iteration: the conv partials of pass
+// c->pend rode in this pass's xbar-sum allreduce, so the convergence test of
+// that pass runs here, one pass late (phbase.py:1498-1553 order otherwise
+// kept).  Converged -> stop = 1 and iter back to that pass; the host then
+// restores the x/y saved before that pass's (speculative) solve.  Used with
+// stop = 2 (limit reached) as the final flush of the last pass.
+__global__ void loop_conv_lagged_kernel(LoopCtl *c, const double *__restrict__ parts,
+                                        const double *__restrict__ cnt, int R, double nproc,
+                                        double *__restrict__ hist, int32_t *ctr) {
+  if (c->stop == 1) return;
+  const int k = c->pend;
+  if (k > 0) {
+    double v = 0.0;
+    for (int r = 0; r < R; ++r) v += parts[r] / cnt[r];
+    v /= nproc;
+    hist[k - 1] = v;
+    c->pend = 0;
+    if (v < c->thresh) {
+      c->stop = 1;
+      c->iter = k;
+    }
+  }
+  if (!c->stop) {
+    ctr[0] = 0;
+    ctr[1] = 0;
+    ctr[2] = 0;
+  }
+}
+
+// Before a pass's solve (several ranks): save x and y (the state the
+// reference keeps if this pass turns out converged) and mark the pass's
+// conv partials pending.
+__global__ void __launch_bounds__(256) loop_backup_kernel(LoopCtl *c, const double *__restrict__ x,
+                                                          double *__restrict__ xb, long nx,
+                                                          const double *__restrict__ y,
+                                                          double *__restrict__ yb, long ny) {
+  if (stopped(c)) return;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nx; i += stride) xb[i] = x[i];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < ny; i += stride) yb[i] = y[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) c->pend = c->iter;
+}
+
 // Single-rank form: the per-reference-rank sums of absdiff over the
 // segments and the conv test in one block (deterministic order).
 __global__ void __launch_bounds__(1024) loop_conv_local_kernel(
@@ -2739,6 +2782,29 @@ int ph_loop_conv(ph_batch_t b, const double *parts, const double *cnt, int32_t R
   if (!(nproc > 0.0)) return fail(PH_EINVAL, "ph_loop_conv: nproc must be > 0");
   hipLaunchKernelGGL(loop_conv_kernel, dim3(1), dim3(1), 0, b->stream, b->d_ctl, parts, cnt, R,
                      nproc, conv_hist, b->d_ctr);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_loop_conv_lagged(ph_batch_t b, const double *parts, const double *cnt, int32_t R,
+                        double nproc, double *conv_hist) {
+  if (!b || !b->loop_on || !parts || !cnt || R <= 0 || !conv_hist)
+    return fail(PH_EINVAL, "ph_loop_conv_lagged: bad arguments (or loop not enabled)");
+  if (!(nproc > 0.0)) return fail(PH_EINVAL, "ph_loop_conv_lagged: nproc must be > 0");
+  hipLaunchKernelGGL(loop_conv_lagged_kernel, dim3(1), dim3(1), 0, b->stream, b->d_ctl, parts, cnt,
+                     R, nproc, conv_hist, b->d_ctr);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_loop_backup(ph_batch_t b, const double *x, double *x_save, int64_t nx, const double *y,
+                   double *y_save, int64_t ny) {
+  if (!b || !b->loop_on || nx < 0 || ny < 0 || (nx && (!x || !x_save)) || (ny && (!y || !y_save)))
+    return fail(PH_EINVAL, "ph_loop_backup: bad arguments (or loop not enabled)");
+  const long mx = (long)std::max(nx, ny);
+  const int grid = (int)std::min<long>(std::max<long>((mx + 255) / 256, 1), 2048);
+  hipLaunchKernelGGL(loop_backup_kernel, dim3(grid), dim3(256), 0, b->stream, b->d_ctl, x, x_save,
+                     (long)nx, y, y_save, (long)ny);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }

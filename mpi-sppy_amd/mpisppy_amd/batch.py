@@ -292,6 +292,18 @@ class DeviceBatch:
                                             parts.numel(), float(nproc),
                                             _native.ptr(conv_hist)), "ph_loop_conv")
 
+    def loop_conv_lagged(self, parts, cnt, nproc, conv_hist):
+        _native.check(self.lib.ph_loop_conv_lagged(self.handle, _native.ptr(parts), _native.ptr(cnt),
+                                                   parts.numel(), float(nproc),
+                                                   _native.ptr(conv_hist)), "ph_loop_conv_lagged")
+
+    def loop_backup(self, x_save, y_save):
+        """Save x and y before this pass's solve (several-rank device loop)."""
+        _native.check(self.lib.ph_loop_backup(self.handle, _native.ptr(self.x), _native.ptr(x_save),
+                                              self.x.numel(), _native.ptr(self.y),
+                                              _native.ptr(y_save), self.y.numel()),
+                      "ph_loop_backup")
+
     def loop_status(self):
         """(stop, iter, not-optimal solves, solves, PDHG iters sum, max, polished,
         cached); synchronises.  stop: 0 running, 1 converged, 2 iteration limit."""

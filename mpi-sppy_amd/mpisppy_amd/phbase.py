@@ -88,7 +88,6 @@ class PHBase(SPBase):
         self.slot_k = torch.as_tensor(self.slot_k_host, **i32)
         self.slot_s0 = torch.as_tensor(self.slot_s0_host, **i32)
         self.slot_s1 = torch.as_tensor(self.slot_s1_host, **i32)
-        self.xsums = torch.zeros(2 * self.G, **f64)
         self.absdiff = torch.zeros(S, **f64)
         self.obj_buf = torch.zeros(S, **f64)
         self.seg_all = torch.tensor([0, S], **i32)
@@ -108,7 +107,12 @@ class PHBase(SPBase):
         self.ref_n_proc = R
         self.conv_seg = torch.tensor(seg, **i32)
         self.conv_cnt = np.array([max(len(sl), 1) * K for sl in slices], dtype=np.float64)
-        self.conv_parts = torch.zeros(R, **f64)
+        # one buffer [xbar sums 2G | conv partials R]: with several ranks the
+        # device loop allreduces both in one collective (conv one pass late)
+        self.xconv = torch.zeros(2 * self.G + R, **f64)
+        self.xsums = self.xconv[:2 * self.G]
+        self.conv_parts = self.xconv[2 * self.G:]
+        self._x_save = self._y_save = None
         self.conv_cnt_dev = torch.as_tensor(self.conv_cnt, **f64)
         # the same weights per local scenario, 1/cnt[r(s)]/R (fused W + conv)
         wconv = np.zeros(S)
@@ -505,12 +509,20 @@ class PHBase(SPBase):
             b.loop_update_w_conv(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
                                  self.xsqbar, self.W, self.absdiff, self.conv_w, self.conv_hist)
         else:
-            self.comm.allreduce_(self.xsums)
+            # one collective per pass: this pass's xbar sums and the previous
+            # pass's conv partials; the previous pass's convergence test runs
+            # now and, if it stops, the host restores the x/y saved before
+            # that pass's solve (run_device_loop)
+            self.comm.allreduce_(self.xconv)
+            b.loop_conv_lagged(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc,
+                               self.conv_hist)
             b.update_w(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
                        self.xsqbar, self.W, self.absdiff)
             b.segment_sum(self.absdiff, None, self.conv_seg, self.conv_parts)
-            self.comm.allreduce_(self.conv_parts)
-            b.loop_conv(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc, self.conv_hist)
+            if self._x_save is None:
+                self._x_save = torch.empty_like(b.x)
+                self._y_save = torch.empty_like(b.y)
+            b.loop_backup(self._x_save, self._y_save)
         b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
 
     def run_device_loop(self, start_iter, iter_limit, convthresh, chunk=None):
@@ -560,6 +572,19 @@ class PHBase(SPBase):
                                            it_max, npol - prev[1]))
                 if stop:
                     break
+            if self.comm.size > 1:
+                # the last pass's conv partials (limit reached), then the
+                # reference's state at a convergence break: x/y of before the
+                # solve that the lagged test showed should not have run
+                self.comm.allreduce_(self.conv_parts)
+                b.loop_conv_lagged(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc,
+                                   self.conv_hist)
+                st = b.loop_status()
+                stop, it = st[0], st[1]
+                nonopt = nonopt or st[2]
+                if stop == 1 and self._x_save is not None:
+                    b.x.copy_(self._x_save)
+                    b.y.copy_(self._y_save)
         finally:
             b.loop_enable(False)
             b.loop_set_xbar(None, None, None, None, None)

@@ -89,6 +89,29 @@ class CPUBatch:
         if v < c["thresh"]:
             c["stop"] = 1
 
+    def loop_conv_lagged(self, parts, cnt, nproc, conv_hist):
+        c = self._ctl
+        if c["stop"] == 1:
+            return
+        k = c.get("pend", 0)
+        if k > 0:
+            v = 0.0
+            for r in range(parts.numel()):
+                v += float(parts[r]) / float(cnt[r])
+            v /= nproc
+            conv_hist[k - 1] = v
+            c["pend"] = 0
+            if v < c["thresh"]:
+                c["stop"] = 1
+                c["iter"] = k
+
+    def loop_backup(self, x_save, y_save):
+        if self._stopped():
+            return
+        x_save.copy_(self.x)
+        y_save.copy_(self.y)
+        self._ctl["pend"] = self._ctl["iter"]
+
     def loop_status(self):
         c = self._ctl
         return (c["stop"], c["iter"], *c["acc"])

@@ -315,7 +315,7 @@ def test_host_loop_device_loop_and_graphs_agree():
         assert _rel(w, w0) < 1e-9
 
 
-def _gpu_rank_worker(rank, world, port, q):
+def _gpu_rank_worker(rank, world, port, q, convthresh):
     """One PH rank on cuda:0 (both ranks share the box's single GPU; the
     collectives go over gloo with host staging, the kernels are the N>1
     device-loop path: update_w, segment_sum, loop_conv between allreduces)."""
@@ -333,7 +333,7 @@ def _gpu_rank_worker(rank, world, port, q):
         from mpisppy_amd.opt.ph import PH
         from mpisppy_amd.examples import farmer
         names = [f"scen{i}" for i in range(30)]
-        opts = _opts(PHIterLimit=40, defaultPHrho=1.0, convthresh=1e-4)
+        opts = _opts(PHIterLimit=40, defaultPHrho=1.0, convthresh=convthresh)
         ph = PH(dict(opts), names, farmer.scenario_creator)
         conv, eobj, tb = ph.ph_main()
         xbar = ph.xbar.view(ph.K, ph.S_loc)[:, 0].cpu().numpy().tolist()
@@ -342,11 +342,14 @@ def _gpu_rank_worker(rank, world, port, q):
         torch.distributed.destroy_process_group()
 
 
-def test_two_ranks_on_gpu_match_oracle():
+@pytest.mark.parametrize("convthresh", [1e-4, 1.0])
+def test_two_ranks_on_gpu_match_oracle(convthresh):
     """The multi-rank device path on the GPU: farmer S=30 split 15/15 over two
-    ranks (sputils.py:625-628), xbar sums and conv partials allreduced every
-    iteration; iterations, conv, Eobj, trivial bound and xbar vs the oracle
-    run on 2 reference ranks."""
+    ranks (sputils.py:625-628), xbar sums and the previous pass's conv
+    partials allreduced together every iteration; iterations, conv, Eobj,
+    trivial bound and xbar vs the oracle run on 2 reference ranks.
+    convthresh 1e-4 ends at the iteration limit (40), 1.0 breaks on
+    convergence at iteration 25 (the lagged test and the x/y restore)."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -355,7 +358,8 @@ def test_two_ranks_on_gpu_match_oracle():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gpu_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gpu_rank_worker, args=(r, 2, port, q, convthresh))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)
@@ -364,9 +368,10 @@ def test_two_ranks_on_gpu_match_oracle():
         assert p.exitcode == 0
     assert res[0][6] == [f"scen{i}" for i in range(15)]
     assert res[1][6] == [f"scen{i}" for i in range(15, 30)]
-    opts = _opts(PHIterLimit=40, defaultPHrho=1.0, convthresh=1e-4)
+    opts = _opts(PHIterLimit=40, defaultPHrho=1.0, convthresh=convthresh)
     orc = OraclePH(dict(opts), [om.farmer(f"scen{i}") for i in range(30)], n_proc=2)
     oc, oe, ot = orc.ph_main()
+    assert orc.iters == (40 if convthresh < 1e-2 else 25)
     for rank, conv, eobj, tb, iters, xbar, _ in res:
         assert iters == orc.iters
         assert abs(conv - oc) / abs(oc) < 1e-3

@@ -132,6 +132,55 @@ def test_two_rank_gloo_hydro_matches_oracle():
         assert abs(tb - ot) < 1e-8 * abs(ot)
 
 
+def _farmer_worker(rank, world, port, q, convthresh):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "mpi-sppy_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mpisppy_amd.examples import farmer
+        names = [f"scen{i}" for i in range(30)]
+        opts = _opts(PHIterLimit=40, convthresh=convthresh)
+        ph, conv, eobj, tb = _run_ph(opts, names, farmer.scenario_creator)
+        hist = ph.conv_hist[:ph._PHIter].cpu().numpy().tolist()
+        q.put((rank, conv, eobj, tb, ph._PHIter, hist))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("convthresh", [1e-4, 1.0])
+def test_two_rank_gloo_lagged_conv_matches_oracle(convthresh):
+    """Several ranks: the conv partials ride in the next pass's xbar-sum
+    allreduce (one collective per iteration).  At the limit (1e-4) and on a
+    convergence break at iteration 25 (1.0: the speculative solve is undone)
+    the iteration count, conv history, Eobj (evaluated at the stale x) and
+    trivial bound equal the oracle on 2 reference ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_farmer_worker, args=(r, 2, port, q, convthresh))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    orc = OraclePH(_opts(PHIterLimit=40, convthresh=convthresh),
+                   [om.farmer(f"scen{i}") for i in range(30)], n_proc=2)
+    oc, oe, ot = orc.ph_main()
+    assert orc.iters == (40 if convthresh < 1e-2 else 25)
+    for rank, conv, eobj, tb, iters, hist in res:
+        assert iters == orc.iters
+        assert abs(conv - oc) < 1e-6 * abs(oc)
+        assert abs(hist[-1] - oc) < 1e-6 * abs(oc)
+        assert abs(eobj - oe) < 1e-7 * abs(oe)
+        assert abs(tb - ot) < 1e-8 * abs(ot)
+
+
 def test_wxbar_csv_round_trip_and_checks(tmp_path):
     """utils/wxbarutils: the reference's csv formats, round trip of W and
     xbar, missing-variable and dual-feasibility errors (wxbarutils.py:212-261)."""
