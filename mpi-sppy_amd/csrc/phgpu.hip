@@ -14,6 +14,8 @@
 //  * the nonanticipativity kernels (xbar sums, W update, convergence sums)
 //    stream the scenario-fastest [k][s] arrays with coalesced FP64 loads.
 #include <hip/hip_runtime.h>
+#include <type_traits>
+#include <cstdlib>
 
 #include <cmath>
 #include <cstdint>
@@ -2642,13 +2644,32 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     a.hint = b->d_hint;
     a.hint_ok = b->d_hint_ok;
     a.wl = b->d_wl;
-    constexpr int WPB = 4, SPW = 1;
     a.wl2 = b->d_wl2;
-    const size_t as_lds =
-        sizeof(double) * WPB * (SPW * ((size_t)b->CW + 4 * b->n + 3 * b->m) + WAVE);
-    const int per_block = WPB * SPW;
-    hipLaunchKernelGGL((active_set_kernel<WPB, SPW>), dim3((b->S + per_block - 1) / per_block),
-                       dim3(WPB * WAVE), as_lds, b->stream, a);
+    // waves per block x scenarios per wave (PHGPU_AS_GEOM = 41|42|81|22|12;
+    // measurement hook, default 4x1)
+    static const int geom = [] {
+      const char *e = std::getenv("PHGPU_AS_GEOM");
+      return e ? std::atoi(e) : 41;
+    }();
+    auto launch_as = [&](auto wpb_c, auto spw_c) {
+      constexpr int WPB = decltype(wpb_c)::value, SPW = decltype(spw_c)::value;
+      const size_t as_lds =
+          sizeof(double) * WPB * (SPW * ((size_t)b->CW + 4 * b->n + 3 * b->m) + WAVE);
+      const int per_block = WPB * SPW;
+      hipLaunchKernelGGL((active_set_kernel<WPB, SPW>), dim3((b->S + per_block - 1) / per_block),
+                         dim3(WPB * WAVE), as_lds, b->stream, a);
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
+    switch (geom) {
+      case 42: launch_as(I4{}, I2{}); break;
+      case 81: launch_as(I8{}, I1{}); break;
+      case 22: launch_as(I2{}, I2{}); break;
+      case 12: launch_as(I1{}, I2{}); break;
+      default: launch_as(I4{}, I1{}); break;
+    }
     HIP_OK(hipGetLastError());
     if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
     // the misses: register Gauss-Jordan polish; what it cannot finish goes
