@@ -1,14 +1,16 @@
 """Per-kernel HBM bytes per launch from rocprofv3 PMC passes of bench.py.
 
-    python tools/pmc_summary.py FETCH_DIR WRITE_DIR STATS_DIR OUT.json SCENS_PER_RANK CROPS
+    python tools/pmc_summary.py FETCH_DIR WRITE_DIR STATS_DIR OUT.json SCENS_PER_RANK CROPS [WINDOW]
 
 FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
 output directories (separate passes, csv).  FETCH_SIZE and WRITE_SIZE are in
 kB per dispatch; per MI355X_MICROARCH.md (HBM section) FETCH_SIZE on gfx950
 reports half the bytes of coalesced reads, so it is doubled here.
 STATS_DIR: the `--kernel-trace --stats` run (kernel time per launch).
-Only the solve kernels of the steady PH iterations are kept: the first 25%
-of each kernel's launches (warmup, Iter0) are skipped.
+Only the last WINDOW launches of each kernel are kept (default 20 = bench.py's
+--steps): with --tol-run 0 --hbm-crops 0 they are the eagerly launched PH
+iterations whose HIP-event times and polish/PDHG counts give the bench line's
+`achieved`, so traffic and algorithmic bytes describe the same launches.
 """
 import csv
 import glob
@@ -27,7 +29,7 @@ def short(name):
     return None
 
 
-def per_kernel(d, counter):
+def per_kernel(d, counter, window):
     f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
     vals = {}
     for r in csv.DictReader(open(f)):
@@ -36,15 +38,16 @@ def per_kernel(d, counter):
             vals.setdefault(k, []).append(float(r["Counter_Value"]))
     out = {}
     for k, v in vals.items():
-        v = v[len(v) // 4:]
+        v = v[-window:]
         out[k] = sum(v) / len(v) if v else None
     return out
 
 
 def main():
     fd, wd, sd, outp, spr, crops = sys.argv[1:7]
-    fetch = per_kernel(fd, "FETCH_SIZE")
-    write = per_kernel(wd, "WRITE_SIZE")
+    window = int(sys.argv[7]) if len(sys.argv) > 7 else 20
+    fetch = per_kernel(fd, "FETCH_SIZE", window)
+    write = per_kernel(wd, "WRITE_SIZE", window)
     times = {}
     f = glob.glob(os.path.join(sd, "*kernel_trace.csv"))[0]
     for r in csv.DictReader(open(f)):
@@ -54,14 +57,16 @@ def main():
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) + "
                      "--kernel-trace --stats of `python bench.py --tol-run 0 --no-cpu-baseline`",
            "fetch_correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section)",
-           "scenarios_per_rank": int(spr), "crops_multiplier": int(crops), "kernels": {}}
+           "scenarios_per_rank": int(spr), "crops_multiplier": int(crops),
+           "window": f"last {window} launches of each kernel (the bench's event-timed iterations)",
+           "kernels": {}}
     for k in KERNELS:
         if k not in fetch and k not in write:
             continue
         fk = fetch.get(k)
         wk = write.get(k)
         t = times.get(k, [])
-        t = t[len(t) // 4:]
+        t = t[-window:]
         hbm = None
         if fk is not None and wk is not None:
             hbm = round((2.0 * fk + wk) * 1024.0)
