@@ -294,3 +294,26 @@ def test_hub_with_lagrangian_and_xhat_spokes_closes_the_gap():
     assert hub.BestOuterBound <= ef + 1e-6 * abs(ef) <= hub.BestInnerBound + 2e-6 * abs(ef)
     assert hub.compute_gap() <= 0.01
     assert hub_opt._PHIter < 50
+
+
+def test_bound_solves_use_tight_tolerance():
+    """post_solve_bound and the Lagrangian spoke solve at bound_pdhg_tol
+    (default 1e-12) unless the caller's solver options set pdhg_tol; PH
+    solves keep the iterk options (bound solves)."""
+    from mpisppy_amd.examples import farmer
+    names = [f"scen{i}" for i in range(6)]
+    ph, conv, eobj, tb = _run_ph(_opts(PHIterLimit=3), names, farmer.scenario_creator)
+    seen = []
+    orig = ph.batch.solve
+
+    def spy(*a, **kw):
+        seen.append(kw.get("tol"))
+        return orig(*a, **kw)
+
+    ph.batch.solve = spy
+    ph.post_solve_bound()
+    ph.post_solve_bound(solver_options={"pdhg_tol": 1e-9})
+    ph.PHoptions["bound_pdhg_tol"] = 1e-11
+    ph.post_solve_bound()
+    ph.solve_loop(solver_options=ph.PHoptions["iterk_solver_options"])
+    assert seen == [1e-12, 1e-9, 1e-11, 1e-9]
