@@ -139,6 +139,13 @@ def pmc_traffic(kname, S_loc, c):
     return None, None
 
 
+def _red_dev():
+    """Device of the timing max-reductions: the GPU under RCCL, host under gloo."""
+    if dist.is_initialized() and dist.get_backend() == "gloo":
+        return "cpu"
+    return "cuda"
+
+
 def hbm_config(args, world, farmer, PH, opts):
     """F3: farmer c=--hbm-crops, --scens scenarios per rank.  Iter0, one
     warmup iteration, then --hbm-steps PH iterations through the device loop
@@ -173,7 +180,7 @@ def hbm_config(args, world, farmer, PH, opts):
     n_t, as_ms, po_ms, pd_ms = b.read_timing()
     st = b.loop_status()
     b.set_timing(False)
-    d = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    d = torch.tensor([dt], dtype=torch.float64, device=_red_dev())
     if world > 1:
         dist.all_reduce(d, op=dist.ReduceOp.MAX)
     dt = float(d.item())
@@ -243,7 +250,10 @@ def run():
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        # BENCH_DIST_BACKEND=gloo rehearses the multi-rank path with several
+        # ranks on one GPU (RCCL refuses two ranks per device); default RCCL
+        dist.init_process_group(os.environ.get("BENCH_DIST_BACKEND", "nccl")
+                                if torch.cuda.is_available() else "gloo")
 
     import mpisppy_amd
     mpisppy_amd.disable_tictoc_output()
@@ -280,7 +290,7 @@ def run():
         dist.barrier()
     dt_local = time.perf_counter() - t0
     st1 = b.loop_status()
-    dts = torch.tensor([dt_local], dtype=torch.float64, device="cuda")
+    dts = torch.tensor([dt_local], dtype=torch.float64, device=_red_dev())
     if world > 1:
         dist.all_reduce(dts, op=dist.ReduceOp.MAX)
     dt = float(dts.item())
@@ -352,7 +362,7 @@ def run():
         ph2.iterk_loop()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t1
-        w = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        w = torch.tensor([wall], dtype=torch.float64, device=_red_dev())
         if world > 1:
             dist.all_reduce(w, op=dist.ReduceOp.MAX)
         eobj = ph2.post_loops()
