@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/phgpu.h"
+#include "kkt_symbolic.h"
 
 #define PHGPU_VERSION "phgpu 0.1 gfx950"
 
@@ -1989,6 +1990,8 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
   }
 }
 
+#include "solve_mid.inc"
+
 // ------------------------------------------------------------------------
 // nonanticipativity kernels (scenario-fastest, coalesced)
 // ------------------------------------------------------------------------
@@ -2292,6 +2295,18 @@ struct ph_batch {
   int32_t *d_c_pb = nullptr, *d_c_pos = nullptr, *d_c_len = nullptr;
   bool bound = false;
   int per = 1, block = 64, ext = 0;
+  // mid-size path (solve_mid): geometry, symbolic KKT analysis, tails
+  bool mid = false;
+  int mblock = 0, mpc = 0, mpr = 0;
+  KktSymbolic sym;
+  int32_t *d_sym = nullptr;   // every int32 array of the symbolic analysis + tails
+  MidArgs md{};
+  int mid_lds_doubles = 0;    // LDS carve of solve_mid (doubles)
+  size_t mid_lds_bytes = 0;
+  double *d_ws = nullptr;     // global polish workspace (when it does not fit in LDS)
+  int mid_grid = 0, mid_pgrid = 0;  // resident blocks of the PDHG / polish phase kernels
+  int32_t *d_mlist = nullptr;  // [5][S] phase work lists
+  int32_t *d_mctr = nullptr;   // [16] list counts (0..4) and queue counters (8..13)
 };
 
 namespace {
@@ -2363,9 +2378,142 @@ void build_chunks(int lines, const std::vector<int32_t> &ptr, std::vector<int32_
   pb[lines] = (int32_t)pos.size();
 }
 
+// Mid-size geometry: one block of BLOCK threads per scenario, PC columns
+// and PR rows per thread (instances listed in DISPATCH_MID).
+bool pick_mid(int n, int m, int *blk, int *pc, int *pr) {
+  const int mx = n > m ? n : m;
+  for (int B : {64, 128, 256, 512})
+    if (mx <= B) {
+      *blk = B;
+      *pc = *pr = 1;
+      return true;
+    }
+  const int c = (n + 1023) / 1024, r = (m + 1023) / 1024;
+  if (c > 3 || r > 3) return false;
+  *blk = 1024;
+  *pc = c > 0 ? c : 1;
+  *pr = r > 0 ? r : 1;
+  return true;
+}
+
+#define MID_CASE(BLK, PCC, PRR, ...)                                                 \
+  else if (b->mblock == BLK && b->mpc == PCC && b->mpr == PRR) {                    \
+    constexpr int B_ = BLK, C_ = PCC, R_ = PRR;                                     \
+    __VA_ARGS__;                                                                    \
+  }
+#define DISPATCH_MID(...)                                                          \
+  do {                                                                             \
+    if (false) {}                                                                  \
+    MID_CASE(64, 1, 1, __VA_ARGS__) MID_CASE(128, 1, 1, __VA_ARGS__)               \
+    MID_CASE(256, 1, 1, __VA_ARGS__) MID_CASE(512, 1, 1, __VA_ARGS__)              \
+    MID_CASE(1024, 1, 1, __VA_ARGS__) MID_CASE(1024, 2, 1, __VA_ARGS__)            \
+    MID_CASE(1024, 1, 2, __VA_ARGS__) MID_CASE(1024, 2, 2, __VA_ARGS__)            \
+    MID_CASE(1024, 3, 1, __VA_ARGS__) MID_CASE(1024, 3, 2, __VA_ARGS__)            \
+    MID_CASE(1024, 1, 3, __VA_ARGS__) MID_CASE(1024, 2, 3, __VA_ARGS__)            \
+    MID_CASE(1024, 3, 3, __VA_ARGS__)                                              \
+    else return fail(PH_EINVAL, "internal: no mid-size kernel instance");          \
+  } while (0)
+
+// Tails of the lines longer than LINE_D for a BLOCK-thread geometry:
+// grouped by the owner's wave (line l is owned by thread l % BLOCK, slot
+// l / BLOCK), see Tails.
+void build_tails(int lines, const int32_t *ptr, int BLOCK, std::vector<int32_t> &wp,
+                 std::vector<int32_t> &tb, std::vector<int32_t> &ln, std::vector<int32_t> &bb,
+                 std::vector<int32_t> &tpos) {
+  const int NW = BLOCK / WAVE;
+  std::vector<std::vector<int>> per_wave(NW);
+  for (int l = 0; l < lines; ++l)
+    if (ptr[l + 1] - ptr[l] > LINE_D) per_wave[(l % BLOCK) / WAVE].push_back(l);
+  wp.assign(NW + 1, 0);
+  tb.assign(1, 0);
+  ln.clear();
+  bb.clear();
+  tpos.clear();
+  for (int w = 0; w < NW; ++w) {
+    for (int l : per_wave[w]) {
+      ln.push_back((l % BLOCK) % WAVE);
+      bb.push_back(l / BLOCK);
+      for (int p = ptr[l] + LINE_D; p < ptr[l + 1]; ++p) tpos.push_back(p);
+      tb.push_back((int32_t)tpos.size());
+    }
+    wp[w + 1] = (int32_t)ln.size();
+  }
+}
+
 }  // namespace
 
 static LoopCtl *loop_ctl(const ph_batch *b) { return b->loop_on ? b->d_ctl : nullptr; }
+
+// Symbolic analysis of the KKT pattern, the tails of long lines and the
+// LDS plan of the mid-size path; uploads the index arrays (one buffer).
+static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx,
+                     const std::vector<int32_t> &col_ptr) {
+  if (!pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr))
+    return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns; the "
+                           "on-chip solver does not cover it");
+  if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx))
+    return fail(PH_ENUM, "ph_batch_create: KKT symbolic analysis failed");
+  const KktSymbolic &y = b->sym;
+  std::vector<int32_t> rwp, rtb, rln, rbb, rtp, cwp, ctb, cln, cbb, ctp;
+  build_tails(b->m, row_ptr, b->mblock, rwp, rtb, rln, rbb, rtp);
+  build_tails(b->n, col_ptr.data(), b->mblock, cwp, ctb, cln, cbb, ctp);
+  std::vector<const std::vector<int32_t> *> parts = {
+      &y.pos, &y.Lcp, &y.Lri, &y.Lcl, &y.Lrp, &y.Lrc, &y.Lrq, &y.lvp, &y.lvc, &y.lep, &y.lee,
+      &y.ecp, &y.ec1, &y.ec2, &y.eck, &y.apos, &y.arow,
+      &rwp, &rtb, &rln, &rbb, &rtp, &cwp, &ctb, &cln, &cbb, &ctp};
+  std::vector<size_t> off;
+  std::vector<int32_t> all;
+  for (auto *v : parts) {
+    off.push_back(all.size());
+    all.insert(all.end(), v->begin(), v->end());
+    all.resize((all.size() + 3) & ~size_t(3), 0);
+  }
+  int rc = dalloc(&b->d_sym, all.size());
+  if (rc) return rc;
+  HIP_OK(hipMemcpy(b->d_sym, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  const int32_t *d = b->d_sym;
+  int q = 0;
+  KktDev &kd = b->md.kd;
+  kd.N = y.N;
+  kd.nnzL = y.nnzL;
+  kd.NL = y.NL;
+  kd.pos = d + off[q++]; kd.Lcp = d + off[q++]; kd.Lri = d + off[q++]; kd.Lcl = d + off[q++];
+  kd.Lrp = d + off[q++]; kd.Lrc = d + off[q++]; kd.Lrq = d + off[q++];
+  kd.lvp = d + off[q++]; kd.lvc = d + off[q++]; kd.lep = d + off[q++]; kd.lee = d + off[q++];
+  kd.ecp = d + off[q++]; kd.ec1 = d + off[q++]; kd.ec2 = d + off[q++]; kd.eck = d + off[q++];
+  kd.apos = d + off[q++]; kd.arow = d + off[q++];
+  Tails &tr = b->md.tr, &tc = b->md.tc;
+  tr.ntail = (int)rtp.size();
+  tr.wp = d + off[q++]; tr.tb = d + off[q++]; tr.ln = d + off[q++]; tr.b = d + off[q++];
+  tr.tpos = d + off[q++];
+  tc.ntail = (int)ctp.size();
+  tc.wp = d + off[q++]; tc.tb = d + off[q++]; tc.ln = d + off[q++]; tc.b = d + off[q++];
+  tc.tpos = d + off[q++];
+  // LDS plan (doubles): see the carve at the top of solve_mid
+  auto up2 = [](long v) { return (v + 1) & ~1L; };
+  auto up4 = [](long v) { return (v + 3) & ~3L; };
+  const int nw = b->mblock / WAVE;
+  tr.nlong = (int)rln.size();
+  tc.nlong = (int)cln.size();
+  auto meta = [&](int nlong) { return (long)nw + 1 + nlong + 1 + 2L * nlong; };
+  const long carve = 6 * up2(b->n) + 6 * up2(b->m) + MAX_WAVES * 10 + up2(tr.ntail) +
+                     up2(tc.ntail) +
+                     (up4(tr.ntail) + up4(tc.ntail) + up4(meta(tr.nlong)) + up4(meta(tc.nlong))) / 2;
+  const long ws = up2(y.nnzL) + 3 * up2(y.N);
+  if ((carve + ws + 2) * 8 <= 160 * 1024) {
+    b->mid_lds_doubles = (int)(carve + ws);
+    b->md.ws_g = nullptr;
+    b->md.ws_stride = 0;
+  } else {
+    if ((carve + 2) * 8 > 160 * 1024)
+      return fail(PH_EINVAL, "ph_batch_create: scenario does not fit in LDS");
+    b->mid_lds_doubles = (int)carve;
+    b->md.ws_stride = ws;  // the workspace goes to HBM once the grid is known
+  }
+  b->mid_lds_bytes = sizeof(double) * ((size_t)b->mid_lds_doubles + 2);
+  b->mid = true;
+  return PH_OK;
+}
 
 extern "C" {
 
@@ -2402,12 +2550,21 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
   build_chunks(n, col_ptr, c_pb, c_pos, c_len);
   b->xr = (int)r_pos.size();
   b->xc = (int)c_pos.size();
-  if (!pick_geometry(n, m, b->xr, b->xc, &b->block, &b->per, &b->ext)) {
+  // scaling-kernel geometry (lines per thread); the one-wave scenarios
+  // (n + m <= POLISH_MAX) keep pdhg_kernel<64,1,E> with the active-set cache,
+  // everything larger goes to the mid-size path (solve_mid)
+  if (!pick_geometry(n, m, 0, 0, &b->block, &b->per, &b->ext)) {
     delete b;
-    return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns (or too many "
-                           "long rows/columns); the on-chip PDHG kernel does not cover it");
+    return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns; the "
+                           "on-chip solver does not cover it");
   }
+  const bool small = b->block == WAVE && b->per == 1 && n + m <= POLISH_MAX &&
+                     pick_geometry(n, m, b->xr, b->xc, &b->block, &b->per, &b->ext);
   int rc = 0;
+  if (!small && (rc = mid_setup(b, row_ptr, col_idx, col_ptr))) {
+    ph_batch_destroy(b);
+    return rc;
+  }
   if ((rc = dalloc(&b->d_row_ptr, m + 1)) || (rc = dalloc(&b->d_col_idx, nnz)) ||
       (rc = dalloc(&b->d_col_ptr, n + 1)) || (rc = dalloc(&b->d_csc_row, nnz)) ||
       (rc = dalloc(&b->d_csc_k, nnz)) || (rc = dalloc(&b->d_slot_of_col, n)) ||
@@ -2471,7 +2628,7 @@ static size_t polish_lds_bytes(const ph_batch *b) {
          sizeof(int32_t) * ((size_t)(b->m + 1) + 3 * (size_t)b->nnz + (b->n + 1) + 2 * WAVE);
 }
 static bool polish_fits(const ph_batch *b) {
-  return b->block == WAVE && b->per == 1 && b->n + b->m <= POLISH_MAX;
+  return !b->mid && b->block == WAVE && b->per == 1 && b->n + b->m <= POLISH_MAX;
 }
 static size_t solve_lds_bytes(const ph_batch *b) {
   size_t d = (size_t)b->n + b->m + b->xr + b->xc + MAX_WAVES * 10;
@@ -2505,7 +2662,7 @@ int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const doubl
                        b->S, b->n, b->m, b->nnz, P, vals, b->d_vals_s, b->d_dr, b->d_dc, b->d_eta);
   });
   HIP_OK(hipGetLastError());
-  if (polish_fits(b)) {
+  if (polish_fits(b) || b->mid) {
     if (!b->d_sb) {
       int rc = dalloc(&b->d_sb, (size_t)b->S * (4 * b->n + 3 * b->m));
       if (rc) return rc;
@@ -2574,6 +2731,114 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
   return PH_OK;
 }
 
+}  // extern "C"
+
+// ph_pdhg_solve for the mid-size path: a fixed sequence of phase kernels
+// over shrinking work lists (a fixed launch sequence, so the device loop can
+// replay it as a graph):
+//   [warm start]  polish (all scenarios, from the warm start's active set)
+//   PDHG  (the rest; hands a trial point on once its KKT error <= 1e-4)
+//   polish (those trial points)   PDHG (hand on at 1e-6)   polish
+//   PDHG  (to tolerance or the iteration limit)
+// then the summary kernel.  Without the polish option: one PDHG phase.
+static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
+  a.polish = opts ? opts->polish : 1;
+  a.cache = nullptr;
+  a.wl = nullptr;
+  if (b->mid_grid == 0) {
+    int per_cu = 0, per_cu_p = 0, cus = 0, dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    DISPATCH_MID({
+      HIP_OK(hipFuncSetAttribute((const void *)mid_kernel<B_, C_, R_>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)b->mid_lds_bytes));
+      HIP_OK(hipFuncSetAttribute((const void *)mid_polish_kernel<B_, C_, R_>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)b->mid_lds_bytes));
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mid_kernel<B_, C_, R_>, B_,
+                                                          b->mid_lds_bytes));
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, mid_polish_kernel<B_, C_, R_>,
+                                                          B_, b->mid_lds_bytes));
+    });
+    if (per_cu < 1 || per_cu_p < 1)
+      return fail(PH_EINVAL, "ph_pdhg_solve: the mid-size kernels cannot be resident");
+    b->mid_grid = std::min(b->S, per_cu * std::max(1, cus));
+    b->mid_pgrid = std::min(b->S, per_cu_p * std::max(1, cus));
+    const int wg = b->S;  // one block per scenario: the workspace slice of block b
+    if (b->md.ws_stride > 0) {
+      int rc = dalloc(&b->d_ws, (size_t)wg * b->md.ws_stride);
+      if (rc) return rc;
+      b->md.ws_g = b->d_ws;
+    }
+    int rc = 0;
+    if ((rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) || (rc = dalloc(&b->d_mctr, 16))) return rc;
+  }
+  HIP_OK(hipMemsetAsync(b->d_mctr, 0, 16 * sizeof(int32_t), b->stream));
+  hipEvent_t *tev = nullptr;
+  if (b->timing) {
+    if (b->ev_used + 4 > b->ev.size()) {
+      for (int i = 0; i < 4; ++i) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreate(&e));
+        b->ev.push_back(e);
+      }
+    }
+    tev = &b->ev[b->ev_used];
+    b->ev_used += 4;
+    HIP_OK(hipEventRecord(tev[0], b->stream));
+  }
+  int32_t *L[5], *C = b->d_mctr, *Q = b->d_mctr + 8;
+  for (int i = 0; i < 5; ++i) L[i] = b->d_mlist + (size_t)i * b->S;
+  auto pdhg = [&](const int32_t *in, const int32_t *cin, int32_t *out, int32_t *cout, int32_t *q,
+                  double exit_err, int first) -> int {
+    const MidPhase ph{in, cin, out, cout, q, exit_err, first, 0};
+    DISPATCH_MID({
+      hipLaunchKernelGGL((mid_kernel<B_, C_, R_>), dim3(b->S), dim3(B_), b->mid_lds_bytes,
+                         b->stream, a, b->md, ph, b->mid_lds_doubles);
+    });
+    HIP_OK(hipGetLastError());
+    return PH_OK;
+  };
+  auto polish = [&](const int32_t *in, const int32_t *cin, int32_t *out, int32_t *cout, int32_t *q,
+                    int mode) -> int {
+    const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode};
+    DISPATCH_MID({
+      hipLaunchKernelGGL((mid_polish_kernel<B_, C_, R_>), dim3(b->S), dim3(B_),
+                         b->mid_lds_bytes, b->stream, a, b->md, ph, b->mid_lds_doubles);
+    });
+    HIP_OK(hipGetLastError());
+    return PH_OK;
+  };
+  int rc = 0;
+  const int32_t *in = nullptr, *cin = nullptr;
+  if (a.polish && a.warm) {
+    if ((rc = polish(nullptr, nullptr, L[0], C + 0, Q + 0, 0))) return rc;
+    in = L[0];
+    cin = C + 0;
+  }
+  if (tev) {
+    HIP_OK(hipEventRecord(tev[1], b->stream));
+    HIP_OK(hipEventRecord(tev[2], b->stream));
+  }
+  if (a.polish) {
+    if ((rc = pdhg(in, cin, L[1], C + 1, Q + 1, POLISH_START, 1)) ||
+        (rc = polish(L[1], C + 1, L[2], C + 2, Q + 2, 1)) ||
+        (rc = pdhg(L[2], C + 2, L[3], C + 3, Q + 3, POLISH_START * 1e-2, 0)) ||
+        (rc = polish(L[3], C + 3, L[4], C + 4, Q + 4, 1)) ||
+        (rc = pdhg(L[4], C + 4, L[1], C + 5, Q + 5, 0.0, 0)))
+      return rc;
+  } else if ((rc = pdhg(in, cin, L[1], C + 1, Q + 1, 0.0, 1))) {
+    return rc;
+  }
+  if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
+  const int post_g = (b->loop_on && b->loop_xa.x == a.x) ? b->loop_xa.G : 0;
+  hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, a.status,
+                     a.iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+extern "C" {
+
 int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double *xbar,
                   double w_on, double prox_on, double *x, double *y, double *omega,
                   int32_t *status, int32_t *iters, double *pobj, double *dbound,
@@ -2614,13 +2879,14 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.ctl = loop_ctl(b);
   a.prof = b->d_prof;
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
+  if (b->mid) return mid_solve(b, a, opts);
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
   if (b->pdhg_grid == 0) {
     int per_cu = 0, cus = 0, dev = 0;
     HIP_OK(hipGetDevice(&dev));
     HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    DISPATCH_GEOM(b->block, b->per, b->ext, {
+    DISPATCH_EXT(64, 1, b->ext, {
       HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pdhg_kernel<B_, P_, E_>, B_, lds));
     });
     b->pdhg_grid = std::max(1, per_cu) * std::max(1, cus);
@@ -2687,7 +2953,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   // behind the cache and the polish the PDHG list is short (usually empty):
   // a small grid drains it from the queue and costs little when empty
   const int grid = std::min(b->S, (a.cache && a.warm) ? std::min(b->pdhg_grid, 64) : b->pdhg_grid);
-  DISPATCH_GEOM(b->block, b->per, b->ext, {
+  DISPATCH_EXT(64, 1, b->ext, {
     hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(grid), dim3(B_), lds, b->stream, a);
   });
   HIP_OK(hipGetLastError());
@@ -2936,7 +3202,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_sb, b->d_part,
-                  b->d_ctl,
+                  b->d_ctl, b->d_sym, b->d_ws, b->d_mlist, b->d_mctr,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

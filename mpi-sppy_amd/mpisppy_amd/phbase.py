@@ -92,7 +92,9 @@ class PHBase(SPBase):
         self.obj_buf = torch.zeros(S, **f64)
         self.seg_all = torch.tensor([0, S], **i32)
         self.scal = torch.zeros(1, **f64)
-        self.w_coeff = None
+        # variable probabilities (spbase.py:369-400): W mask, or None
+        self.w_coeff = None if self.w_coeff_host is None else \
+            torch.as_tensor(self.w_coeff_host.reshape(-1), **f64)
         # convergence_diff: the reference's rank slices (ref_n_proc ranks)
         R = int(self.PHoptions.get("ref_n_proc", self.n_proc))
         if R < 1 or R > len(self.all_scenario_names):
@@ -411,11 +413,15 @@ class PHBase(SPBase):
         cols = torch.as_tensor(self.batch_data.nonant_cols.astype(np.int64), device=self.device)
         return x.index_select(0, cols).cpu().numpy()
 
-    def gather_var_values_to_rank0(self):
-        """spbase.py: {(scenario_name, nonant var name): value} on rank 0."""
+    def gather_var_values_to_rank0(self, get_zero_prob_values=False):
+        """spbase.py:519-543: {(scenario_name, nonant var name): value} on
+        rank 0; zero-probability nonants give None unless asked for."""
         vals = self._local_nonant_values()
         names = self.nonant_names()
-        local = {(sn, names[k]): float(vals[k, s])
+        zero = np.zeros_like(self.prob_coeff_host, dtype=bool) if self.w_coeff_host is None \
+            else (self.prob_coeff_host == 0.0)
+        local = {(sn, names[k]): (None if zero[k, s] and not get_zero_prob_values
+                                  else float(vals[k, s]))
                  for s, sn in enumerate(self.local_scenario_names) for k in range(self.K)}
         allv = self.comm.gather_object(local)
         if self.cylinder_rank != 0:

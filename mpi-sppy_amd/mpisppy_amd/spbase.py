@@ -85,6 +85,7 @@ class SPBase:
         self._create_node_slots()
         self._verify_nonant_lengths()
         self.is_minimizing = self.batch_data.sense == "min"
+        self._use_variable_probability_setter(options.get("verbose", False))
         self._spcomm = None
 
     # ---------------------------------------------------------------- setup
@@ -190,6 +191,98 @@ class SPBase:
                 slot_s1[base + i] = s1 + 1
         self.gid_host = gid
         self.slot_k_host, self.slot_s0_host, self.slot_s1_host = slot_k, slot_s0, slot_s1
+
+    def _nonant_slot_of(self, s, key):
+        """Nonant slot k of scenario s named by ``key``: a nonant VarData of
+        the scenario's model, ``id()`` of one (the reference's form,
+        ``spbase.py:386-388``), or a nonant variable name."""
+        d = self.batch_data
+        if not hasattr(self, "_slot_by_name"):
+            names = self.nonant_names()
+            self._slot_by_name = {nm: k for k, nm in enumerate(names)}
+            self._col2slot = {int(c): k for k, c in enumerate(d.nonant_cols)}
+        if isinstance(key, str):
+            if key not in self._slot_by_name:
+                raise KeyError(f"variable_probability: {key!r} is not a nonant")
+            return self._slot_by_name[key]
+        models = d.models
+        if models is None:
+            raise TypeError("variable_probability: without per-scenario models, name nonants "
+                            "by variable name")
+        mdl = models[s]
+        from . import repn
+        if isinstance(key, int):
+            ids = getattr(mdl, "_mpisppy_amd_nonant_ids", None)
+            if ids is None:
+                ids = {}
+                for node in mdl._mpisppy_node_list:
+                    for vd in node.nonant_vardata_list:
+                        ids[id(vd)] = self._col2slot[repn.column_of(mdl, vd)]
+                mdl._mpisppy_amd_nonant_ids = ids
+            if key not in ids:
+                raise KeyError("variable_probability: id is not a nonant of the scenario")
+            return ids[key]
+        col = repn.column_of(mdl, key)
+        if col not in self._col2slot:
+            raise KeyError("variable_probability: variable is not a nonant")
+        return self._col2slot[col]
+
+    def _use_variable_probability_setter(self, verbose=False):
+        """spbase.py:369-400: per-variable probabilities.
+
+        ``variable_probability(scenario, **variable_probability_kwargs)``
+        returns [(var, prob)] for the scenario (var: VarData, its id(), or a
+        nonant name).  The probability REPLACES prob_coeff of that nonant
+        (so Compute_Xbar weights it), and a zero probability masks the
+        nonant's W (``w_coeff``, applied by Update_W, phbase.py:246-251).
+        As in the reference, touching any nonant of a tree node turns the
+        whole node into per-variable values (defaults kept for the rest)."""
+        d = self.batch_data
+        self.w_coeff_host = None
+        self.has_variable_probability = self.variable_probability is not None
+        if self.variable_probability is None:
+            return
+        kw = self.options.get("variable_probability_kwargs", dict())
+        wc = np.ones((d.K, d.S))
+        didit = 0
+        for s, (sname, view) in enumerate(self.local_scenarios.items()):
+            target = view.model if view.model is not None else view
+            for key, prob in self.variable_probability(target, **kw):
+                k = self._nonant_slot_of(s, key)
+                self.prob_coeff_host[k, s] = float(prob)
+                if prob == 0:
+                    wc[k, s] = 0.0
+                didit += 1
+        self.w_coeff_host = wc
+        if verbose and self.cylinder_rank == 0:
+            print("variable_probability set", didit, "and skipped", d.K * d.S - didit)
+        if "do_not_check_variable_probabilities" in self.options \
+                and not self.options["do_not_check_variable_probabilities"]:
+            self._check_variable_probabilities_sum(verbose)
+
+    def _check_variable_probabilities_sum(self, verbose):
+        """spbase.py:417-460: per node slot, the sum of prob_coeff over all
+        scenarios of the node must be 1 (within E1_tolerance)."""
+        d = self.batch_data
+        sums = np.zeros(self.G)
+        np.add.at(sums, self.gid_host.reshape(-1), self.prob_coeff_host.reshape(-1))
+        tot = np.asarray(self.comm.allreduce_host(sums.tolist()))
+        bad = np.nonzero(~np.isclose(tot, 1.0, atol=self.E1_tolerance))[0]
+        if bad.size:
+            names = self.nonant_names()
+            slot_of_g = {int(g): int(k) for k, g in zip(np.repeat(np.arange(d.K), d.S),
+                                                         self.gid_host.reshape(-1))}
+            raise RuntimeError("Node conditional probabilities do not sum to 1 for nonants "
+                               + ", ".join(f"{names[slot_of_g[g]]} (sum {tot[g]})" for g in bad))
+        if verbose and self.cylinder_rank == 0:
+            print("Checked variable probability sums")
+
+    def is_zero_prob(self, scenario_model, var):
+        """spbase.py:402-415."""
+        if self.variable_probability is None:
+            return False
+        s = self.local_scenario_names.index(scenario_model.name)
+        return float(self.prob_coeff_host[self._nonant_slot_of(s, var), s]) == 0.0
 
     def _verify_nonant_lengths(self):
         ks = self.comm.allreduce_host([self.batch_data.K, -self.batch_data.K], op="max")

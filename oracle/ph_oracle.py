@@ -22,7 +22,7 @@ def rank_slices(num_scens, n_proc):
 class OraclePH:
     """PH over a list of :class:`oracle.models.OScen` (all scenarios, in order)."""
 
-    def __init__(self, options, scens, n_proc=1):
+    def __init__(self, options, scens, n_proc=1, variable_prob=None):
         self.options = dict(options)
         self.scens = scens
         self.S = len(scens)
@@ -42,6 +42,20 @@ class OraclePH:
             self.prob_coeff.append(pcs)
         rho0 = float(self.options["defaultPHrho"])
         self.K = [len(s.nonant_idx) for s in scens]
+        # per nonant slot weights; variable probabilities (spbase.py:369-400)
+        # replace a slot's prob_coeff and mask its W when zero (phbase.py:246-251)
+        self.pc_slot = []
+        self.w_coeff = []
+        for s, sc in enumerate(scens):
+            pcs = np.concatenate([np.full(len(idx), self.prob_coeff[s][j])
+                                  for j, (nm, cp, idx) in enumerate(sc.nodes)])
+            wc = np.ones(len(pcs))
+            for k, p in (variable_prob or {}).get(s, {}).items():
+                pcs[k] = p
+                if p == 0:
+                    wc[k] = 0.0
+            self.pc_slot.append(pcs)
+            self.w_coeff.append(wc)
         self.W = [np.zeros(k) for k in self.K]           # phbase.py:1113-1115
         self.rho = [np.full(k, rho0) for k in self.K]    # phbase.py:1128-1131
         self.xbar = [np.zeros(k) for k in self.K]        # phbase.py:1622-1632
@@ -116,17 +130,18 @@ class OraclePH:
             accsq = np.zeros(nlen)
             for (s, off, ln, j) in members:
                 xs = self.x[s][self.scens[s].nonant_idx[off:off + ln]]
-                acc += self.prob_coeff[s][j] * xs
-                accsq += self.prob_coeff[s][j] * xs ** 2
+                pc = self.pc_slot[s][off:off + ln]
+                acc += pc * xs
+                accsq += pc * xs ** 2
             for (s, off, ln, j) in members:
                 self.xbar[s][off:off + ln] = acc
                 self.xsqbar[s][off:off + ln] = accsq
 
     def Update_W(self):
-        """phbase.py:224-251 (no variable probabilities)."""
+        """phbase.py:224-251 (W masked by w_coeff after the update)."""
         for s in range(self.S):
             xs = self.x[s][self.scens[s].nonant_idx]
-            self.W[s] = self.W[s] + self.rho[s] * (xs - self.xbar[s])
+            self.W[s] = (self.W[s] + self.rho[s] * (xs - self.xbar[s])) * self.w_coeff[s]
 
     def convergence_diff(self):
         """phbase.py:254-276: sum over ranks of local mean |x-xbar|, / n_proc."""

@@ -317,3 +317,46 @@ def test_bound_solves_use_tight_tolerance():
     ph.post_solve_bound()
     ph.solve_loop(solver_options=ph.PHoptions["iterk_solver_options"])
     assert seen == [1e-12, 1e-9, 1e-11, 1e-9]
+
+
+def _vprob(S):
+    """Slot 0 of even scenarios carries probability 2/S, of odd ones 0 (its
+    W is masked); every slot still sums to 1 over the scenarios."""
+    def variable_probability(scen, first_name=None):
+        s = int(scen.name[4:])
+        return [(first_name, 2.0 / S if s % 2 == 0 else 0.0)]
+    return variable_probability
+
+
+def test_variable_probability_matches_oracle():
+    """spbase.py:369-400 / phbase.py:246-251: per-variable probabilities
+    replace prob_coeff in Compute_Xbar and zero-probability nonants have W
+    masked; host flow (CPU stand-in batch) against the oracle."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    from cpu_batch import CPUBatch
+    S = 6
+    names = [f"scen{i}" for i in range(S)]
+    probe = PH(_opts(), names, farmer.scenario_creator)
+    first = probe.nonant_names()[0]
+    opts = _opts(PHIterLimit=5, variable_probability_kwargs={"first_name": first},
+                 do_not_check_variable_probabilities=False)
+    ph = PH(dict(opts), names, farmer.scenario_creator, variable_probability=_vprob(S))
+    ph.batch = CPUBatch(ph.batch_data)
+    conv, eobj, tb = ph.ph_main()
+    vp = {s: {0: (2.0 / S if s % 2 == 0 else 0.0)} for s in range(S)}
+    orc = OraclePH(opts, [om.farmer(n) for n in names], variable_prob=vp)
+    oc, oe, ot = orc.ph_main()
+    W = ph.W.view(ph.K, ph.S_loc).numpy().T
+    assert np.allclose(W, np.array(orc.W), rtol=1e-9, atol=1e-9)
+    assert np.all(W[1::2, 0] == 0.0) and np.any(W[0::2, 0] != 0.0)
+    xb = ph.xbar.view(ph.K, ph.S_loc)[:, 0].numpy()
+    assert np.allclose(xb, orc.xbar[0], rtol=1e-9, atol=1e-9)
+    assert abs(conv - oc) < 1e-9 * abs(oc) and abs(eobj - oe) < 1e-9 * abs(oe)
+    v = ph.gather_var_values_to_rank0()
+    assert v[("scen1", first)] is None and v[("scen0", first)] is not None
+    assert ph.gather_var_values_to_rank0(get_zero_prob_values=True)[("scen1", first)] is not None
+    # a setter whose probabilities do not sum to 1 is rejected when checked
+    with pytest.raises(RuntimeError, match="do not sum to 1"):
+        PH(dict(opts), names, farmer.scenario_creator,
+           variable_probability=lambda sc, first_name=None: [(first_name, 0.5)])
