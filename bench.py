@@ -205,7 +205,57 @@ def hbm_config(args, world, farmer, PH, opts):
                                  "scenario on chip, so frac > 1 is possible"}}
 
 
+def _spawn_ranks(n, cpu):
+    """`bench.py --gpus N` without a launcher: this parent (which has not
+    touched the GPU) starts N rank processes, one per GPU, with the
+    torch.distributed env (127.0.0.1 rendezvous), hands rank 0 the CPU
+    baseline it measured, relays rank 0's JSON line and returns the worst
+    exit code."""
+    import socket
+    import subprocess
+    import tempfile
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cpu_file = None
+    if cpu is not None:
+        fd, cpu_file = tempfile.mkstemp(prefix="bench_cpu_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(cpu, f)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if cpu_file:
+            env["BENCH_CPU_BASELINE_FILE"] = cpu_file
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else None))
+    out0 = procs[0].communicate()[0]
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    if cpu_file:
+        os.unlink(cpu_file)
+    sys.stdout.write(out0.decode())
+    sys.stdout.flush()
+    return max(abs(rc) for rc in rcs)
+
+
 def main():
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    pre, _ = ap.parse_known_args()
+    if world == 0 and pre.gpus > 1:
+        # no launcher: measure the CPU baseline here (its workers fork before
+        # any GPU use), then one process per GPU
+        real_stdout = sys.stdout
+        sys.stdout = sys.stderr
+        try:
+            cpu = None if pre.no_cpu_baseline else _cpu_baseline_from_args()
+        finally:
+            sys.stdout = real_stdout
+        sys.exit(_spawn_ranks(pre.gpus, cpu))
     # everything but the final JSON line goes to stderr
     real_stdout = sys.stdout
     sys.stdout = sys.stderr
@@ -217,7 +267,7 @@ def main():
         print(json.dumps(out), flush=True)
 
 
-def run():
+def _parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -236,17 +286,31 @@ def run():
     ap.add_argument("--hbm-crops", type=int, default=100,
                     help="crops_multiplier of the HBM-bound companion config (F3); 0 = skip")
     ap.add_argument("--hbm-steps", type=int, default=5)
-    args = ap.parse_args()
+    return ap
 
+
+def _cpu_baseline_from_args():
+    args = _parser().parse_args()
+    if args.no_cpu_baseline:
+        return None
+    try:
+        return cpu_baseline(args.crops, args.cpu_sample, args.cpu_seconds, args.cpu_cores)
+    except Exception as e:  # the baseline must not kill the GPU number
+        return {"value": None, "error": repr(e)}
+
+
+def run():
+    args = _parser().parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None  # CPU baseline first: its worker processes fork before any GPU use
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            cpu = cpu_baseline(args.crops, args.cpu_sample, args.cpu_seconds, args.cpu_cores)
-        except Exception as e:  # the baseline must not kill the GPU number
-            cpu = {"value": None, "error": repr(e)}
+    if os.environ.get("BENCH_CPU_BASELINE_FILE"):
+        if rank == 0:
+            with open(os.environ["BENCH_CPU_BASELINE_FILE"]) as f:
+                cpu = json.load(f)
+    elif rank == 0 and world == 1:
+        cpu = _cpu_baseline_from_args()
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
     if world > 1:
@@ -254,6 +318,10 @@ def run():
         # ranks on one GPU (RCCL refuses two ranks per device); default RCCL
         dist.init_process_group(os.environ.get("BENCH_DIST_BACKEND", "nccl")
                                 if torch.cuda.is_available() else "gloo")
+        if dist.get_world_size() != world:
+            raise RuntimeError(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
+        print(f"[bench] rank {rank}: {dist.get_world_size()} ranks over "
+              f"{dist.get_backend()}", file=sys.stderr)
 
     import mpisppy_amd
     mpisppy_amd.disable_tictoc_output()
@@ -296,6 +364,9 @@ def run():
     dt = float(dts.item())
     # (run_device_loop resets the device counters: st1 counts the timed steps)
     n_solves = st1[3]
+    if n_solves != ph.S_loc * args.steps:
+        raise RuntimeError(f"timed region solved {n_solves} scenarios, expected "
+                           f"{ph.S_loc} x {args.steps}")
     tot_iters = float(st1[4])
     n_polished = float(st1[6])
     n_cached = float(st1[7])

@@ -27,6 +27,7 @@
 
 struct KktSymbolic {
   int n = 0, m = 0, N = 0, nnzL = 0, NL = 0;
+  int chain0 = 0;  // levels chain0 .. NL-1 hold one column each (the top of the tree)
   long ncontrib = 0;
   std::vector<int32_t> pos;              // [N] vertex -> permuted index
   std::vector<int32_t> Lcp, Lri, Lcl;    // CSC of the strict lower triangle of L; column of entry
@@ -156,6 +157,8 @@ struct KktSymbolic {
       std::vector<int32_t> fill(lvp.begin(), lvp.end() - 1);
       for (int c = 0; c < N; ++c) lvc[fill[level[c]]++] = c;
     }
+    chain0 = NL;
+    while (chain0 > 0 && lvp[chain0] - lvp[chain0 - 1] == 1) --chain0;
     lep.assign(NL + 1, 0);
     lee.clear();
     lee.reserve(nnzL);

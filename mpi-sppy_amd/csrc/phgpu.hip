@@ -1318,6 +1318,44 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     __syncthreads();
   }
 
+  // ---- not optimal: the Lagrangian dual bound of the sign-feasible y (a
+  // valid outer bound whatever the state of convergence; -inf when a
+  // reduced cost pushes a one-sided column to its infinite bound)
+  double safe_bound = 0.0;
+  if (stat != PH_STATUS_OPTIMAL) {
+    __syncthreads();
+    double v[1] = {0.0};
+#pragma unroll
+    for (int b = 0; b < RPT; ++b) {
+      int i = tid + b * T;
+      if (i < m) {
+        double y = Y[b];
+        if (!isfinite(RL[b])) y = fmin(y, 0.0);
+        if (!isfinite(RU[b])) y = fmax(y, 0.0);
+        ys[i] = y;
+        v[0] += y > 0.0 ? y * RL[b] : (y < 0.0 ? y * RU[b] : 0.0);
+      }
+    }
+    __syncthreads();
+    CL.dots(ys, part_c, DOT);
+#pragma unroll
+    for (int b = 0; b < CPT; ++b) {
+      int j = tid + b * T;
+      if (j < n) {
+        const double rj = G[b] - DOT[b];
+        if (Q[b] > 0.0) {
+          const double xq = clampd(-rj / Q[b], L[b], U[b]);
+          v[0] += 0.5 * Q[b] * xq * xq + rj * xq;
+        } else if (rj > 0.0) {
+          v[0] += rj * L[b];
+        } else if (rj < 0.0) {
+          v[0] += rj * U[b];
+        }
+      }
+    }
+    block_sum<1>(v, red);
+    safe_bound = v[0] + cst;
+  }
   // ---- write back (unscaled, scenario-fastest)
 #pragma unroll
   for (int b = 0; b < CPT; ++b) {
@@ -1334,7 +1372,7 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     a.status[s] = stat;
     a.iters[s] = it;
     a.pobj[s] = out_pobj;
-    a.dbound[s] = out_dobj;
+    a.dbound[s] = stat == PH_STATUS_OPTIMAL ? out_dobj : safe_bound;
     a.diag[PH_DIAG_W * s + 0] = d_ep;
     a.diag[PH_DIAG_W * s + 1] = d_ed;
     a.diag[PH_DIAG_W * s + 2] = d_eg;
@@ -2296,13 +2334,15 @@ struct ph_batch {
   bool bound = false;
   int per = 1, block = 64, ext = 0;
   // mid-size path (solve_mid): geometry, symbolic KKT analysis, tails
-  bool mid = false;
+  bool mid = false;        // the mid-size path solves this batch
+  bool mid_ready = false;  // its symbolic data is set up (also for the one-wave rescue)
   int mblock = 0, mpc = 0, mpr = 0;
   KktSymbolic sym;
   int32_t *d_sym = nullptr;   // every int32 array of the symbolic analysis + tails
   MidArgs md{};
   int mid_lds_doubles = 0;    // LDS carve of solve_mid (doubles)
-  size_t mid_lds_bytes = 0;
+  size_t mid_lds_bytes = 0;   // LDS of the PDHG phase kernel
+  size_t mid_plds_bytes = 0;  // LDS of the polish phase kernel
   double *d_ws = nullptr;     // global polish workspace (when it does not fit in LDS)
   int mid_grid = 0, mid_pgrid = 0;  // resident blocks of the PDHG / polish phase kernels
   int32_t *d_mlist = nullptr;  // [5][S] phase work lists
@@ -2477,6 +2517,11 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   kd.N = y.N;
   kd.nnzL = y.nnzL;
   kd.NL = y.NL;
+  kd.chain0 = y.chain0;
+  {  // PHGPU_KKT_DELTA: measurement hook for the polish regularisation
+    const char *e = std::getenv("PHGPU_KKT_DELTA");
+    b->md.delta = e ? std::atof(e) : KKT_DELTA;
+  }
   kd.pos = d + off[q++]; kd.Lcp = d + off[q++]; kd.Lri = d + off[q++]; kd.Lcl = d + off[q++];
   kd.Lrp = d + off[q++]; kd.Lrc = d + off[q++]; kd.Lrq = d + off[q++];
   kd.lvp = d + off[q++]; kd.lvc = d + off[q++]; kd.lep = d + off[q++]; kd.lee = d + off[q++];
@@ -2496,22 +2541,23 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   tr.nlong = (int)rln.size();
   tc.nlong = (int)cln.size();
   auto meta = [&](int nlong) { return (long)nw + 1 + nlong + 1 + 2L * nlong; };
-  const long carve = 6 * up2(b->n) + 6 * up2(b->m) + MAX_WAVES * 10 + up2(tr.ntail) +
-                     up2(tc.ntail) +
-                     (up4(tr.ntail) + up4(tc.ntail) + up4(meta(tr.nlong)) + up4(meta(tc.nlong))) / 2;
-  const long ws = up2(y.nnzL) + 3 * up2(y.N);
-  if ((carve + ws + 2) * 8 <= 160 * 1024) {
-    b->mid_lds_doubles = (int)(carve + ws);
+  const long common = up2(b->n) + up2(b->m) + MAX_WAVES * 10 + up2(tr.ntail) + up2(tc.ntail) +
+                      (up4(tr.ntail) + up4(tc.ntail) + up4(meta(tr.nlong)) + up4(meta(tc.nlong))) / 2;
+  const long state = 5 * up2(b->n) + 5 * up2(b->m);  // the PDHG kernel's per-line data
+  const long ws = up2(y.nnzL) + 3 * up2(y.N);         // the polish workspace
+  if ((common + state + 2) * 8 > 160 * 1024)
+    return fail(PH_EINVAL, "ph_batch_create: scenario does not fit in LDS");
+  b->mid_lds_bytes = sizeof(double) * ((size_t)common + state + 2);
+  if ((common + ws + 2) * 8 <= 160 * 1024) {
+    b->mid_plds_bytes = sizeof(double) * ((size_t)common + ws + 2);
     b->md.ws_g = nullptr;
     b->md.ws_stride = 0;
   } else {
-    if ((carve + 2) * 8 > 160 * 1024)
-      return fail(PH_EINVAL, "ph_batch_create: scenario does not fit in LDS");
-    b->mid_lds_doubles = (int)carve;
-    b->md.ws_stride = ws;  // the workspace goes to HBM once the grid is known
+    b->mid_plds_bytes = sizeof(double) * ((size_t)common + 2);
+    b->md.ws_stride = ws;  // the workspace goes to HBM (allocated with the first solve)
   }
-  b->mid_lds_bytes = sizeof(double) * ((size_t)b->mid_lds_doubles + 2);
-  b->mid = true;
+  b->mid_lds_doubles = (int)(common + state);
+  b->mid_ready = true;
   return PH_OK;
 }
 
@@ -2561,10 +2607,15 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
   const bool small = b->block == WAVE && b->per == 1 && n + m <= POLISH_MAX &&
                      pick_geometry(n, m, b->xr, b->xc, &b->block, &b->per, &b->ext);
   int rc = 0;
-  if (!small && (rc = mid_setup(b, row_ptr, col_idx, col_ptr))) {
+  // (one-wave batches set it up too: their rescue polish for scenarios the
+  // one-wave solve leaves at the iteration limit -- degenerate LPs at tight
+  // tolerances, where the register Gauss-Jordan polish meets a singular set)
+  if ((rc = mid_setup(b, row_ptr, col_idx, col_ptr)) && !small) {
     ph_batch_destroy(b);
     return rc;
   }
+  b->mid = !small;
+  if (rc) g_err.clear();
   if ((rc = dalloc(&b->d_row_ptr, m + 1)) || (rc = dalloc(&b->d_col_idx, nnz)) ||
       (rc = dalloc(&b->d_col_ptr, n + 1)) || (rc = dalloc(&b->d_csc_row, nnz)) ||
       (rc = dalloc(&b->d_csc_k, nnz)) || (rc = dalloc(&b->d_slot_of_col, n)) ||
@@ -2733,6 +2784,48 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
 
 }  // extern "C"
 
+// The repaired Lagrangian bound of the scenarios a solve left short of
+// the tolerance (bound_kernel; blocks of the others exit at once).
+static int launch_bound(ph_batch *b, const SolveArgs &a) {
+  if (!b->d_sb) return PH_OK;
+  const size_t lds = sizeof(double) * (((size_t)b->n + 1 & ~(size_t)1) + ((size_t)b->m + 1 & ~(size_t)1) + MAX_WAVES);
+  hipLaunchKernelGGL(bound_kernel<256>, dim3(b->S), dim3(256), lds, b->stream, a);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+// First-use setup of the mid-size kernels: LDS limits, occupancy, the HBM
+// polish workspace (when it does not fit in LDS), the work lists.
+static int mid_init(ph_batch *b) {
+  if (b->mid_grid != 0) return PH_OK;
+  int per_cu = 0, per_cu_p = 0, cus = 0, dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  DISPATCH_MID({
+    HIP_OK(hipFuncSetAttribute((const void *)mid_kernel<B_, C_, R_>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)b->mid_lds_bytes));
+    HIP_OK(hipFuncSetAttribute((const void *)mid_polish_kernel<B_, C_, R_>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)b->mid_plds_bytes));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mid_kernel<B_, C_, R_>, B_,
+                                                        b->mid_lds_bytes));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, mid_polish_kernel<B_, C_, R_>,
+                                                        B_, b->mid_plds_bytes));
+  });
+  if (per_cu < 1 || per_cu_p < 1)
+    return fail(PH_EINVAL, "ph_pdhg_solve: the mid-size kernels cannot be resident");
+  b->mid_grid = std::min(b->S, per_cu * std::max(1, cus));
+  b->mid_pgrid = std::min(b->S, per_cu_p * std::max(1, cus));
+  const int wg = b->S;  // one block per scenario: the workspace slice of block b
+  if (b->md.ws_stride > 0) {
+    int rc = dalloc(&b->d_ws, (size_t)wg * b->md.ws_stride);
+    if (rc) return rc;
+    b->md.ws_g = b->d_ws;
+  }
+  int rc = 0;
+  if ((rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) || (rc = dalloc(&b->d_mctr, 16))) return rc;
+  return PH_OK;
+}
+
 // ph_pdhg_solve for the mid-size path: a fixed sequence of phase kernels
 // over shrinking work lists (a fixed launch sequence, so the device loop can
 // replay it as a graph):
@@ -2745,33 +2838,7 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   a.polish = opts ? opts->polish : 1;
   a.cache = nullptr;
   a.wl = nullptr;
-  if (b->mid_grid == 0) {
-    int per_cu = 0, per_cu_p = 0, cus = 0, dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    DISPATCH_MID({
-      HIP_OK(hipFuncSetAttribute((const void *)mid_kernel<B_, C_, R_>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)b->mid_lds_bytes));
-      HIP_OK(hipFuncSetAttribute((const void *)mid_polish_kernel<B_, C_, R_>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)b->mid_lds_bytes));
-      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mid_kernel<B_, C_, R_>, B_,
-                                                          b->mid_lds_bytes));
-      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, mid_polish_kernel<B_, C_, R_>,
-                                                          B_, b->mid_lds_bytes));
-    });
-    if (per_cu < 1 || per_cu_p < 1)
-      return fail(PH_EINVAL, "ph_pdhg_solve: the mid-size kernels cannot be resident");
-    b->mid_grid = std::min(b->S, per_cu * std::max(1, cus));
-    b->mid_pgrid = std::min(b->S, per_cu_p * std::max(1, cus));
-    const int wg = b->S;  // one block per scenario: the workspace slice of block b
-    if (b->md.ws_stride > 0) {
-      int rc = dalloc(&b->d_ws, (size_t)wg * b->md.ws_stride);
-      if (rc) return rc;
-      b->md.ws_g = b->d_ws;
-    }
-    int rc = 0;
-    if ((rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) || (rc = dalloc(&b->d_mctr, 16))) return rc;
-  }
+  if (int rc = mid_init(b)) return rc;
   HIP_OK(hipMemsetAsync(b->d_mctr, 0, 16 * sizeof(int32_t), b->stream));
   hipEvent_t *tev = nullptr;
   if (b->timing) {
@@ -2789,8 +2856,8 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   int32_t *L[5], *C = b->d_mctr, *Q = b->d_mctr + 8;
   for (int i = 0; i < 5; ++i) L[i] = b->d_mlist + (size_t)i * b->S;
   auto pdhg = [&](const int32_t *in, const int32_t *cin, int32_t *out, int32_t *cout, int32_t *q,
-                  double exit_err, int first) -> int {
-    const MidPhase ph{in, cin, out, cout, q, exit_err, first, 0};
+                  double exit_err, int first, int hand_at_limit) -> int {
+    const MidPhase ph{in, cin, out, cout, q, exit_err, first, 0, hand_at_limit};
     DISPATCH_MID({
       hipLaunchKernelGGL((mid_kernel<B_, C_, R_>), dim3(b->S), dim3(B_), b->mid_lds_bytes,
                          b->stream, a, b->md, ph, b->mid_lds_doubles);
@@ -2800,10 +2867,10 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   };
   auto polish = [&](const int32_t *in, const int32_t *cin, int32_t *out, int32_t *cout, int32_t *q,
                     int mode) -> int {
-    const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode};
+    const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode, 0, 0};
     DISPATCH_MID({
       hipLaunchKernelGGL((mid_polish_kernel<B_, C_, R_>), dim3(b->S), dim3(B_),
-                         b->mid_lds_bytes, b->stream, a, b->md, ph, b->mid_lds_doubles);
+                         b->mid_plds_bytes, b->stream, a, b->md, ph, b->mid_lds_doubles);
     });
     HIP_OK(hipGetLastError());
     return PH_OK;
@@ -2820,15 +2887,18 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     HIP_OK(hipEventRecord(tev[2], b->stream));
   }
   if (a.polish) {
-    if ((rc = pdhg(in, cin, L[1], C + 1, Q + 1, POLISH_START, 1)) ||
+    // (the last polish takes the scenarios the final PDHG left at its limit)
+    if ((rc = pdhg(in, cin, L[1], C + 1, Q + 1, POLISH_START, 1, 0)) ||
         (rc = polish(L[1], C + 1, L[2], C + 2, Q + 2, 1)) ||
-        (rc = pdhg(L[2], C + 2, L[3], C + 3, Q + 3, POLISH_START * 1e-2, 0)) ||
+        (rc = pdhg(L[2], C + 2, L[3], C + 3, Q + 3, POLISH_START * 1e-2, 0, 0)) ||
         (rc = polish(L[3], C + 3, L[4], C + 4, Q + 4, 1)) ||
-        (rc = pdhg(L[4], C + 4, L[1], C + 5, Q + 5, 0.0, 0)))
+        (rc = pdhg(L[4], C + 4, L[1], C + 5, Q + 5, 0.0, 0, 1)) ||
+        (rc = polish(L[1], C + 5, L[0], C + 6, Q + 6, 1)))
       return rc;
-  } else if ((rc = pdhg(in, cin, L[1], C + 1, Q + 1, 0.0, 1))) {
+  } else if ((rc = pdhg(in, cin, L[1], C + 1, Q + 1, 0.0, 1, 0))) {
     return rc;
   }
+  if (int rc2 = launch_bound(b, a)) return rc2;
   if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
   const int post_g = (b->loop_on && b->loop_xa.x == a.x) ? b->loop_xa.G : 0;
   hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, a.status,
@@ -2957,6 +3027,20 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(grid), dim3(B_), lds, b->stream, a);
   });
   HIP_OK(hipGetLastError());
+  if (a.polish && b->mid_ready) {
+    // rescue: the quasi-definite LDL' polish (regularised, refined: it copes
+    // with the singular active sets of degenerate LPs) from the final PDHG
+    // point of every scenario left at the iteration limit; blocks of the
+    // others exit at once
+    if (int rc = mid_init(b)) return rc;
+    const MidPhase ph{nullptr, nullptr, nullptr, nullptr, nullptr, 0.0, 0, 1, 0, 1};
+    DISPATCH_MID({
+      hipLaunchKernelGGL((mid_polish_kernel<B_, C_, R_>), dim3(b->S), dim3(B_), b->mid_plds_bytes,
+                         b->stream, a, b->md, ph, b->mid_lds_doubles);
+    });
+    HIP_OK(hipGetLastError());
+  }
+  if (int rc = launch_bound(b, a)) return rc;
   if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
   // device loop: the summary block also advances the iteration, and G
   // more blocks compute the next iteration's Compute_Xbar sums

@@ -164,6 +164,9 @@ class DeviceBatch:
         self.rl = up(data.rl) if self.m else torch.zeros(1, **f64)
         self.ru = up(data.ru) if self.m else torch.zeros(1, **f64)
         h = _native._c_ptr()
+        # the torch stream the library's launches are ordered on (collectives
+        # on the batch's tensors are queued on it too, phbase._allreduce)
+        self.torch_stream = torch.cuda.current_stream(self.dev) if stream is None else stream
         sh = _native.stream_handle(stream)
         self._stream_handle = sh.value or 0
         _native.check(lib.ph_batch_create(h, self.S, self.n, self.m, self.nnz,

@@ -261,21 +261,7 @@ class PHBase(SPBase):
         dt = time.perf_counter() - t0
         self.solve_log.append((self.S_loc, dt, it_sum / max(self.S_loc, 1), it_max,
                                npol + ncache))
-        if nonopt:
-            status = b.status.cpu().numpy()
-            self.scenario_feasible = (status == 0) | (status == 1)
-            nlim = int(np.sum(status == 1))
-        else:
-            if not self._all_feasible:
-                self.scenario_feasible = np.ones(self.S_loc, dtype=bool)
-            nlim = 0
-        self._all_feasible = not nonopt
-        if nlim and gripe:
-            print(f"[{type(self).__name__}] {nlim} scenario(s) stopped at the PDHG "
-                  f"iteration limit ({kw['max_iters']})")
-        if gripe and not np.all(self.scenario_feasible):
-            for i in np.nonzero(~self.scenario_feasible)[0]:
-                print(f"[{type(self).__name__}] Solve failed for scenario {self.local_scenario_names[i]}")
+        self._set_feasibility(nonopt, gripe, kw["max_iters"])
         if dtiming:
             allt = self.comm.allgather_object(dt)
             if self.cylinder_rank == 0:
@@ -290,16 +276,50 @@ class PHBase(SPBase):
         elif dis_prox:
             self._reenable_prox()
 
+    def _set_feasibility(self, nonopt, gripe, max_iters):
+        """phbase.py:959-989: scenario_feasible from the per-scenario
+        statuses.  Only a solve that reached the KKT tolerance counts: a
+        scenario stopped at the PDHG iteration limit (status 1) holds an
+        iterate, not a solution, and reports a safe Lagrangian dual bound
+        (possibly -inf) as its outer bound; statuses 2/3 are certified
+        primal / dual infeasibility."""
+        if nonopt:
+            status = self.batch.status.cpu().numpy()
+            self.scenario_feasible = status == 0
+        elif not self._all_feasible:
+            self.scenario_feasible = np.ones(self.S_loc, dtype=bool)
+        self._all_feasible = not nonopt
+        if not (gripe and nonopt):
+            return
+        name = type(self).__name__
+        if self.spcomm is not None:
+            name = type(self.spcomm).__name__
+        why = {1: f"PDHG iteration limit ({max_iters}) reached before the KKT tolerance",
+               2: "primal infeasible", 3: "dual infeasible (unbounded)"}
+        for i in np.nonzero(status != 0)[0]:
+            print(f"[{name}] Solve failed for scenario {self.local_scenario_names[i]}: "
+                  f"{why.get(int(status[i]), 'status %d' % status[i])}")
+
     def _sync(self):
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
     # ---------------------------------------- nonanticipativity updates --
+    def _allreduce(self, t):
+        """Collective on a device tensor, ordered on the batch's stream (the
+        library's kernels run there; under RCCL the collective is queued on
+        torch's current stream)."""
+        ts = getattr(self.batch, "torch_stream", None)
+        if ts is None or not t.is_cuda:
+            return self.comm.allreduce_(t)
+        with torch.cuda.stream(ts):
+            return self.comm.allreduce_(t)
+
     def Compute_Xbar(self, verbose=False):
         """phbase.py:144-221: weighted node sums, Allreduce, broadcast."""
         b = self.batch
         b.xbar_accum(self.prob_coeff, self.slot_k, self.slot_s0, self.slot_s1, self.xsums)
-        self.comm.allreduce_(self.xsums)
+        self._allreduce(self.xsums)
         b.update_w(self.xsums, self.G, self.gid, self.rho, None, self.xbar, self.xsqbar,
                    None, self.absdiff)
         if verbose and self.cylinder_rank == 0:
@@ -316,7 +336,7 @@ class PHBase(SPBase):
         Reproduces the reference's rank slicing for ``ref_n_proc`` ranks
         (default: this run's rank count)."""
         self.batch.segment_sum(self.absdiff, None, self.conv_seg, self.conv_parts)
-        self.comm.allreduce_(self.conv_parts)
+        self._allreduce(self.conv_parts)
         parts = self.conv_parts.cpu().numpy()
         return float(np.sum(parts / self.conv_cnt) / self.ref_n_proc)
 
@@ -330,7 +350,7 @@ class PHBase(SPBase):
         b.eval_objective(self.W, self.rho, self.xbar, self.w_on, self.prox_on, self.obj_buf)
         self.obj_buf.add_(b.const)
         t = self._weighted_sum(self.obj_buf).clone()
-        self.comm.allreduce_(t)
+        self._allreduce(t)
         v = float(t.item())
         return v if self.is_minimizing else -v
 
@@ -345,7 +365,7 @@ class PHBase(SPBase):
         if extra_sum_terms is not None:
             t = torch.cat([t, torch.tensor(list(extra_sum_terms), dtype=torch.float64,
                                            device=t.device)])
-        self.comm.allreduce_(t)
+        self._allreduce(t)
         v = t.cpu().numpy()
         if extra_sum_terms is None:
             return float(v[0])
@@ -469,8 +489,9 @@ class PHBase(SPBase):
             raise RuntimeError(f"Total probability of scenarios was {self.E1} "
                                f"(E1_tolerance = {self.E1_tolerance})")
         feasP = self.feas_prob()
-        if feasP != self.E1:
-            raise RuntimeError(f"Infeasibility detected; E_feas, E1= {feasP} {self.E1}")
+        if feasP != self.E1:  # phbase.py:1421-1427 (the reference quit()s)
+            raise RuntimeError(f"Infeasibility detected; E_feas, E1= {feasP} {self.E1} "
+                               "(a scenario is infeasible or was not solved to tolerance)")
         if self.PH_extensions is not None:
             self.extobject.post_iter0()
         if self.rho_setter is not None:
@@ -519,7 +540,7 @@ class PHBase(SPBase):
             # pass's conv partials; the previous pass's convergence test runs
             # now and, if it stops, the host restores the x/y saved before
             # that pass's solve (run_device_loop)
-            self.comm.allreduce_(self.xconv)
+            self._allreduce(self.xconv)
             b.loop_conv_lagged(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc,
                                self.conv_hist)
             b.update_w(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
@@ -582,7 +603,7 @@ class PHBase(SPBase):
                 # the last pass's conv partials (limit reached), then the
                 # reference's state at a convergence break: x/y of before the
                 # solve that the lagged test showed should not have run
-                self.comm.allreduce_(self.conv_parts)
+                self._allreduce(self.conv_parts)
                 b.loop_conv_lagged(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc,
                                    self.conv_hist)
                 st = b.loop_status()
@@ -595,13 +616,7 @@ class PHBase(SPBase):
             b.loop_enable(False)
             b.loop_set_xbar(None, None, None, None, None)
             self._loop_prev = (0, 0)
-        if nonopt:
-            status = b.status.cpu().numpy()
-            self.scenario_feasible = (status == 0) | (status == 1)
-            if not np.all(self.scenario_feasible):
-                for i in np.nonzero(~self.scenario_feasible)[0]:
-                    print(f"[{type(self).__name__}] Solve failed for scenario "
-                          f"{self.local_scenario_names[i]}")
+        self._set_feasibility(nonopt, True, kw["max_iters"])
         return stop, it
 
     def _graph_ok(self):

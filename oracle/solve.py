@@ -22,7 +22,7 @@ class OracleSolveError(RuntimeError):
     pass
 
 
-def _highs_solve(c, q, A, rl, ru, l, u):
+def _highs_solve(c, q, A, rl, ru, l, u, time_limit=20.0):
     A = sp.csc_matrix(A)
     m, n = A.shape
     lp = hc.HighsLp()
@@ -46,7 +46,7 @@ def _highs_solve(c, q, A, rl, ru, l, u):
     h.setOptionValue("primal_feasibility_tolerance", 1e-10)
     h.setOptionValue("dual_feasibility_tolerance", 1e-10)
     h.setOptionValue("random_seed", 0)
-    h.setOptionValue("time_limit", 20.0)  # a stuck solve fails loudly instead of hanging
+    h.setOptionValue("time_limit", time_limit)  # a stuck solve fails loudly instead of hanging
     h.passModel(lp)
     if q is not None and np.any(q != 0):
         hs = hc.HighsHessian()
@@ -155,6 +155,56 @@ def _basis_polish(c, q, A, rl, ru, l, u, kkt_tol, rounds=10):
             return best
         atl, atu, rtl, rtu = natl, natu, nrtl, nrtu
     return best
+
+
+def _qp_by_cuts(c, q, A, rl, ru, l, u, iters=400):
+    """Approximate prox-QP point by Kelley cutting planes: each quadratic
+    term 1/2 q_j x_j^2 becomes an epigraph column t_j >= q_j a x_j - q_j a^2/2
+    over a growing set of tangent points a, solved as LPs by HiGHS simplex.
+    Used only to seed the active set when HiGHS's own QP solver stalls (its
+    time limit; seen on sslp_15_45_15 prox-QPs); the exact point then comes
+    from the PDAS polish and the KKT check."""
+    A = sp.csr_matrix(A)
+    m, n = A.shape
+    J = np.nonzero(q)[0]
+    k = J.size
+    pts = []
+    for j in J:
+        lo = l[j] if np.isfinite(l[j]) else -1e4
+        hi = u[j] if np.isfinite(u[j]) else 1e4
+        pts.append(list(np.linspace(lo, hi, 33)))
+    x = None
+    global _last_basis
+    for _ in range(iters):
+        rows, cols, vals, lo_, hi_ = [], [], [], [], []
+        r = 0
+        for t, j in enumerate(J):
+            for a in pts[t]:
+                # q a x_j - t_j <= q a^2 / 2
+                rows += [r, r]
+                cols += [j, n + t]
+                vals += [q[j] * a, -1.0]
+                lo_.append(-np.inf)
+                hi_.append(0.5 * q[j] * a * a)
+                r += 1
+        C = sp.coo_matrix((vals, (rows, cols)), shape=(r, n + k)).tocsr()
+        Ax = sp.vstack([sp.hstack([A, sp.csr_matrix((m, k))]), C]).tocsr()
+        st, z, _, _ = _highs_solve(np.concatenate([c, np.ones(k)]), None, Ax,
+                                   np.concatenate([rl, lo_]), np.concatenate([ru, hi_]),
+                                   np.concatenate([l, np.full(k, -np.inf)]),
+                                   np.concatenate([u, np.full(k, np.inf)]))
+        if "Optimal" not in str(st):
+            return x
+        x, tt = z[:n], z[n:]
+        gap = 0.5 * q[J] * x[J] ** 2 - tt
+        if np.max(gap) <= 1e-14 * (1.0 + np.max(np.abs(c))):
+            if _last_basis is not None:  # the original columns' and rows' statuses
+                _last_basis = (_last_basis[0][:n], _last_basis[1][:m])
+            break
+        for t, j in enumerate(J):
+            if gap[t] > 0:
+                pts[t].append(x[j])
+    return x
 
 
 def kkt_residual(x, y, c, q, A, rl, ru, l, u):
@@ -281,10 +331,29 @@ def solve_scenario(c, q, A, rl, ru, l, u, kkt_tol=1e-9):
     passes the KKT check.
     """
     q = np.zeros_like(c) if q is None else np.asarray(q, dtype=np.float64)
-    status, x, rowdual, _ = _highs_solve(c, q, A, rl, ru, l, u)
+    status, x, rowdual, _ = _highs_solve(c, q, A, rl, ru, l, u,
+                                         time_limit=5.0 if np.any(q) else 20.0)
     name = str(status)
     if "Infeasible" in name or "Unbounded" in name:
         return None, None, False
+    if "TimeLimit" in name and np.any(q):
+        xc = _qp_by_cuts(c, q, A, rl, ru, l, u)
+        if xc is None:
+            raise OracleSolveError("HiGHS QP time limit and the cut fallback failed")
+        best = (np.inf, None, None)
+        if _last_basis is not None and _last_basis[0].size == c.size:
+            bp = _basis_polish(c, q, A, rl, ru, l, u, kkt_tol)
+            if bp is not None:
+                best = bp
+                if bp[0] <= kkt_tol:
+                    return bp[1], bp[2], True
+        for tau in (1e-6, 1e-5, 1e-7, 1e-4, 1e-8):
+            err, xp, yp = _pdas(xc, c, q, A, rl, ru, l, u, tau, kkt_tol)
+            if err < best[0]:
+                best = (err, xp, yp)
+            if err <= kkt_tol:
+                return xp, yp, True
+        raise OracleSolveError(f"QP cut fallback polish failed, best KKT residual {best[0]:.3e}")
     if "Optimal" not in name:
         raise OracleSolveError(f"HiGHS status {name}")
     # HiGHS row duals: d(obj)/d(row activity); our y = -rowdual? -> determine

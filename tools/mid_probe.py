@@ -100,7 +100,13 @@ def run_f3(S=10000, c=100, nit=5):
     print(f"F3 Iter0 {t0:.3f}s status {np.bincount(st)} how {np.bincount(dg[:, 4].astype(int))} "
           f"pdhg it p50 {np.percentile(it, 50):.0f} p99 {np.percentile(it, 99):.0f} max {it.max()}",
           flush=True)
+    import ctypes
+    lib = b.lib
+    lib.ph_debug_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    lib.ph_debug_prof.restype = ctypes.c_int32
+    prof = np.zeros(16, dtype=np.int64)
     for k in range(nit):
+        lib.ph_debug_prof(b.handle, 1, None)
         torch.cuda.synchronize()
         t = time.time()
         ph.Compute_Xbar()
@@ -111,8 +117,12 @@ def run_f3(S=10000, c=100, nit=5):
         st = b.status.cpu().numpy()
         it = b.iters.cpu().numpy()
         dg = b.diagnostics()
+        lib.ph_debug_prof(b.handle, 1, prof.ctypes.data_as(ctypes.c_void_p))
+        npol = max(prof[9], 1)
         print(f"F3 PH it {k+1}: {dt*1000:.1f} ms status {np.bincount(st)} how "
-              f"{np.bincount(dg[:, 4].astype(int), minlength=3)} pdhg it mean {it.mean():.1f} max {it.max()}",
+              f"{np.bincount(dg[:, 4].astype(int), minlength=3)} pdhg it mean {it.mean():.1f} max {it.max()}"
+              f" | polish {prof[9]} rounds/pol {prof[10]/npol:.2f} refine/pol {prof[11]/npol:.2f} ok {prof[12]}"
+              f" us/pol: build {prof[15]/npol/100:.1f} factor {prof[13]/npol/100:.1f} solve {prof[14]/npol/100:.1f}",
               flush=True)
 
 
