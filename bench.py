@@ -76,14 +76,13 @@ def _cpu_worker(arg):
             return n, dt
 
 
-def cpu_baseline(c, sample_scens, min_seconds=10.0, cores=16):
+def cpu_subproblem_rate(c, sample_scens, min_seconds=10.0, cores=16):
     """Oracle subproblem engine (HiGHS 1.8 from scipy) timed on this host on a
-    bounded sample of the same workload: the prox-QPs of one PH iteration (W
-    and xbar from an oracle Iter0) for `sample_scens` farmer scenarios, solved
-    sequentially per process like the reference's solve_loop (one rank per
-    core), each process cycling its share for `min_seconds`.
-    Timed on 1 core and on `cores` forked processes.  Runs before anything
-    touches the GPU (the workers are forked)."""
+    bounded sample: the prox-QPs of one PH iteration (W and xbar from an
+    oracle Iter0) for `sample_scens` farmer c=`c` scenarios, solved
+    sequentially per process like the reference's solve_loop, each of
+    `cores` forked processes cycling its share for `min_seconds`.  Runs
+    before anything touches the GPU (the workers are forked)."""
     global _CPU_PROBS
     import multiprocessing as mp
     sys.path.insert(0, ROOT)
@@ -101,22 +100,48 @@ def cpu_baseline(c, sample_scens, min_seconds=10.0, cores=16):
         sc = scens[s]
         probs.append((g, q, sc.A, sc.rl, sc.ru, sc.l, sc.u))
     _CPU_PROBS = probs
-    n1, dt1 = _cpu_worker((0, 1, min_seconds))
-    one = n1 / dt1
     cores = max(1, min(cores, len(os.sched_getaffinity(0)), len(probs)))
-    value, dtm, nm = one, dt1, n1
-    if cores > 1:
-        with mp.get_context("fork").Pool(cores) as pool:
-            res = pool.map(_cpu_worker, [(w, cores, min_seconds) for w in range(cores)])
-        nm = sum(r[0] for r in res)
-        dtm = max(r[1] for r in res)
-        value = nm / dtm
-    return {"value": round(value, 2), "unit": "solves/s", "cores": cores, "kind": "port",
-            "value_1core": round(one, 2),
-            "sample": f"{len(probs)} distinct farmer c={c} PH prox-QP subproblems of one PH "
-                      f"iteration after Iter0, cycled; HiGHS 1.8.0 QP via scipy; {cores} "
-                      f"processes x {dtm:.1f} s ({nm} solves), and 1 process x {dt1:.1f} s "
-                      f"({n1} solves)"}
+    with mp.get_context("fork").Pool(cores) as pool:
+        res = pool.map(_cpu_worker, [(w, cores, min_seconds) for w in range(cores)])
+    nm = sum(r[0] for r in res)
+    dtm = max(r[1] for r in res)
+    return {"value": round(nm / dtm, 2), "unit": "solves/s", "cores": cores, "kind": "port",
+            "sample": f"{len(probs)} distinct farmer c={c} PH prox-QPs of one PH iteration after "
+                      f"Iter0 (HiGHS 1.8.0 QP via scipy, no polish), cycled on {cores} processes "
+                      f"x {dtm:.1f} s ({nm} solves)"}
+
+
+def cpu_baseline(c, scens, convthresh, cores=16, f3_crops=100, f3_sample=64, f3_seconds=8.0):
+    """the oracle PH (oracle/ph_dist.py: phbase.py's
+    Iter0/iterk control flow, exact HiGHS + KKT-polish subproblem solves,
+    Compute_Xbar/convergence_diff allreduces) on `cores` gloo ranks of this
+    host, the same farmer instance and convthresh as the GPU's PH-to-tol
+    run, at `scens` scenarios (a bounded sample of the 10k workload; the GPU
+    runs the same size too, see ph_to_tol_sample).  value = subproblem
+    solves / wall seconds of that run.  Plus a c=`f3_crops` subproblem-rate
+    sample for the F3 companion config."""
+    sys.path.insert(0, ROOT)
+    from oracle import ph_dist
+    cores = max(1, min(cores, len(os.sched_getaffinity(0))))
+    t0 = time.perf_counter()
+    r = ph_dist.run(cores, scens, crops=c, rho=1.0, convthresh=convthresh)
+    wall = time.perf_counter() - t0
+    out = {"value": round(r["subproblem_solves"] / r["seconds_to_tol"], 2), "unit": "solves/s",
+           "cores": cores, "kind": "port",
+           "sample": f"oracle PH (oracle/ph_dist.py) on {cores} gloo ranks, farmer c={c}, "
+                     f"{scens} scenarios, rho 1, convthresh {convthresh}: {r['iterations']} PH "
+                     f"iterations, {r['subproblem_solves']} exact subproblem solves in "
+                     f"{r['seconds_to_tol']:.2f} s (Iter0 {r['seconds_iter0']:.2f} s; "
+                     f"{wall:.1f} s with rank start-up)",
+           "ph_to_tol": {"seconds": round(r["seconds_to_tol"], 3), "ph_iterations": r["iterations"],
+                         "scenarios": scens, "convthresh": convthresh, "final_conv": r["conv"],
+                         "Eobj": r["Eobj"], "trivial_bound": r["trivial_bound"]}}
+    if f3_crops > 0:
+        try:
+            out["f3_subproblems"] = cpu_subproblem_rate(f3_crops, f3_sample, f3_seconds, cores)
+        except Exception as e:  # the F3 sample must not kill the baseline
+            out["f3_subproblems"] = {"value": None, "error": repr(e)}
+    return out
 
 
 def pmc_traffic(kname, S_loc, c):
@@ -209,8 +234,8 @@ def _spawn_ranks(n, cpu):
     """`bench.py --gpus N` without a launcher: this parent (which has not
     touched the GPU) starts N rank processes, one per GPU, with the
     torch.distributed env (127.0.0.1 rendezvous), hands rank 0 the CPU
-    baseline it measured, relays rank 0's JSON line and returns the worst
-    exit code."""
+    baseline it measured; returns the worst exit code and rank 0's JSON
+    line."""
     import socket
     import subprocess
     import tempfile
@@ -224,6 +249,8 @@ def _spawn_ranks(n, cpu):
         with os.fdopen(fd, "w") as f:
             json.dump(cpu, f)
     procs = []
+    # (this process's fd 1 is stderr by now: rank 0's JSON comes back
+    # through a pipe of its own)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -235,12 +262,26 @@ def _spawn_ranks(n, cpu):
     rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
     if cpu_file:
         os.unlink(cpu_file)
-    sys.stdout.write(out0.decode())
-    sys.stdout.flush()
-    return max(abs(rc) for rc in rcs)
+    lines = [ln for ln in out0.decode().splitlines() if ln.startswith("{")]
+    return max(abs(rc) for rc in rcs), (lines[-1] if lines else None)
 
 
 def main():
+    # fd 1 carries the JSON line only: everything else written to stdout, by
+    # this process or by children that inherit it (the CPU baseline's gloo
+    # ranks print from C++), goes to stderr
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+    rc = _main()
+    sys.stdout.flush()
+    if isinstance(rc, str):
+        os.write(json_fd, (rc + "\n").encode())
+        rc = 0
+    os.close(json_fd)
+    sys.exit(rc or 0)
+
+
+def _main():
     world = int(os.environ.get("WORLD_SIZE", "0"))
     ap = argparse.ArgumentParser(add_help=False)
     ap.add_argument("--gpus", type=int, default=1)
@@ -249,22 +290,11 @@ def main():
     if world == 0 and pre.gpus > 1:
         # no launcher: measure the CPU baseline here (its workers fork before
         # any GPU use), then one process per GPU
-        real_stdout = sys.stdout
-        sys.stdout = sys.stderr
-        try:
-            cpu = None if pre.no_cpu_baseline else _cpu_baseline_from_args()
-        finally:
-            sys.stdout = real_stdout
-        sys.exit(_spawn_ranks(pre.gpus, cpu))
-    # everything but the final JSON line goes to stderr
-    real_stdout = sys.stdout
-    sys.stdout = sys.stderr
-    try:
-        out = run()
-    finally:
-        sys.stdout = real_stdout
-    if out is not None:
-        print(json.dumps(out), flush=True)
+        cpu = None if pre.no_cpu_baseline else _cpu_baseline_from_args()
+        rc, line = _spawn_ranks(pre.gpus, cpu)
+        return line if rc == 0 and line else rc
+    out = run()
+    return json.dumps(out) if out is not None else 0
 
 
 def _parser():
@@ -278,8 +308,8 @@ def _parser():
     ap.add_argument("--rho", type=float, default=1.0)
     ap.add_argument("--tol-run", type=int, default=1, help="also time PH to convthresh")
     ap.add_argument("--convthresh", type=float, default=1e-4)
-    ap.add_argument("--cpu-sample", type=int, default=500)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-scens", type=int, default=200,
+                    help="scenarios of the CPU-baseline oracle PH run (and of the GPU run beside it)")
     ap.add_argument("--cpu-cores", type=int, default=16,
                     help="CPU-baseline processes (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -294,7 +324,8 @@ def _cpu_baseline_from_args():
     if args.no_cpu_baseline:
         return None
     try:
-        return cpu_baseline(args.crops, args.cpu_sample, args.cpu_seconds, args.cpu_cores)
+        return cpu_baseline(args.crops, args.cpu_scens, args.convthresh, args.cpu_cores,
+                            args.hbm_crops)
     except Exception as e:  # the baseline must not kill the GPU number
         return {"value": None, "error": repr(e)}
 
@@ -413,13 +444,13 @@ def run():
     cached_frac = n_cached / max(n_solves, 1)
     traffic, traffic_src = pmc_traffic(kname, S_loc, c)
 
-    # PH wall-clock to convergence tolerance (fresh run, same instance)
-    tol_info = None
-    if args.tol_run:
+    # PH wall-clock to convergence tolerance (fresh runs, same instance): the
+    # 10k headline size, and the CPU baseline's sample size beside it
+    def ph_to_tol(S_tol):
         opts2 = dict(opts)
         opts2["convthresh"] = args.convthresh
         opts2["PHIterLimit"] = 5000
-        names2 = [f"scen{i}" for i in range(args.tol_scens)]
+        names2 = [f"scen{i}" for i in range(S_tol)]
         ph2 = PH(opts2, names2, farmer.scenario_creator,
                  scenario_creator_kwargs={"crops_multiplier": c})
         ph2.PH_Prep()
@@ -437,10 +468,15 @@ def run():
         if world > 1:
             dist.all_reduce(w, op=dist.ReduceOp.MAX)
         eobj = ph2.post_loops()
-        tol_info = {"seconds": round(float(w.item()), 4), "ph_iterations": ph2._PHIter,
-                    "convthresh": args.convthresh, "final_conv": ph2.conv,
-                    "trivial_bound": tb, "Eobj": eobj, "scenarios": args.tol_scens,
-                    "n_gpus": world}
+        return {"seconds": round(float(w.item()), 4), "ph_iterations": ph2._PHIter,
+                "convthresh": args.convthresh, "final_conv": ph2.conv,
+                "trivial_bound": tb, "Eobj": eobj, "scenarios": S_tol, "n_gpus": world}
+
+    tol_info = tol_small = None
+    if args.tol_run:
+        tol_info = ph_to_tol(args.tol_scens)
+        if args.cpu_scens != args.tol_scens:
+            tol_small = ph_to_tol(args.cpu_scens)
 
     # companion HBM-bound config: farmer crops_multiplier
     # 100, 10k scenarios per GPU -- the PDHG kernel's regime
@@ -448,8 +484,6 @@ def run():
     if args.hbm_crops > 0:
         f3 = hbm_config(args, world, farmer, PH, opts)
 
-    if cpu is not None and tol_info is not None and cpu.get("value"):
-        cpu["ph_to_tol_projected_s"] = round(tol_info["ph_iterations"] * S / cpu["value"], 1)
 
     if rank == 0:
         value = S * args.steps / dt
@@ -493,6 +527,7 @@ def run():
             "polished_fraction": round(polished_frac, 4),
             "cached_fraction": round(cached_frac, 4),
             "ph_to_tol": tol_info,
+            "ph_to_tol_sample": tol_small,
             "cpu_baseline": cpu,
             "hbm_config": f3,
         }

@@ -296,8 +296,17 @@ __device__ __forceinline__ bool stopped(const LoopCtl *c) {
   return c && *(volatile const int32_t *)&c->stop;
 }
 
+// Primal-weight drift allowed before a reset to omega0, per path.  The
+// mid-size path's degenerate LPs need several decades (F3's 10k Iter0 LPs:
+// at 1e2 seven stall at the 200k limit, at 1e6 all converge within 20k
+// steps); the one-wave path's tight-tolerance bound LPs want the reset (F2
+// post_solve_bound at 1e-12: 1 of 10k at the limit with 1e2, 79 with 1e6).
+constexpr double OMEGA_SPAN_SMALL = 1e2;
+constexpr double OMEGA_SPAN_MID = 1e6;
+
 struct SolveArgs {
   int S, n, m, nnz;
+  double omega_span;  // the primal weight is reset to omega0 once it leaves [omega0/span, omega0*span]
   Pattern P;
   Chunks X;
   const double *vals_s, *dr, *dc, *eta;
@@ -1010,7 +1019,8 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     // warm primal weight, kept within 100x of the data-based weight: carried
     // unclamped across PH iterations it drifts (1e6x seen on farmer) into a
     // regime where FP64 round-off stalls the iteration above 1e-9.
-    if (a.warm && a.omega[s] > 0.0) omega = clampd(a.omega[s], omega0 * 1e-2, omega0 * 1e2);
+    if (a.warm && a.omega[s] > 0.0)
+      omega = clampd(a.omega[s], omega0 / a.omega_span, omega0 * a.omega_span);
   }
   const double eta = a.eta[s];
   const double gam = a.refl;
@@ -1287,7 +1297,7 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     // 100x from the data-based weight is reset (seen stalling on farmer warm
     // starts at ~1e-8 relative KKT, in both directions)
     const bool reset = it > 0 && ((it + 1) % 8192) < chk &&
-                       (omega > 1e2 * omega0 || omega < 1e-2 * omega0);
+                       (omega > a.omega_span * omega0 || omega * a.omega_span < omega0);
     if (reset) {
       omega = omega0;
       restart = true;
@@ -2919,6 +2929,13 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   if (b->K && (!W || !rho || !xbar)) return fail(PH_EINVAL, "ph_pdhg_solve: null W/rho/xbar");
   SolveArgs a;
   a.S = b->S; a.n = b->n; a.m = b->m; a.nnz = b->nnz;
+  {  // PHGPU_OMEGA_SPAN: measurement hook (F3's degenerate LPs stall at 1e2)
+    static const double span = [] {
+      const char *e = std::getenv("PHGPU_OMEGA_SPAN");
+      return e ? std::atof(e) : 0.0;
+    }();
+    a.omega_span = span > 0.0 ? span : (b->mid ? OMEGA_SPAN_MID : OMEGA_SPAN_SMALL);
+  }
   a.P = Pattern{b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k};
   a.X = Chunks{b->xr, b->xc, b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   a.vals_s = b->d_vals_s; a.dr = b->d_dr; a.dc = b->d_dc; a.eta = b->d_eta;

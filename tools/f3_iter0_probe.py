@@ -47,5 +47,8 @@ print(f"Iter0 {dt:.2f}s  not optimal {bad.size}  iters p50 {np.percentile(it, 50
 for s in bad[:40]:
     print("  scen", s, "iters", it[s], "ep %.2e ed %.2e eg %.2e r %.2e" % tuple(dg[s, :4]))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+X = b.x.view(b.n, b.S).cpu().numpy()
+Y = b.y.view(-1, b.S).cpu().numpy()
 np.savez(os.path.join(ROOT, "gpurun_out", f"f3_iter0_c{C}.npz"), bad=bad, iters=it, status=st,
-         diag=dg, dbound=b.dbound.cpu().numpy(), pobj=b.pobj.cpu().numpy())
+         diag=dg, dbound=b.dbound.cpu().numpy(), pobj=b.pobj.cpu().numpy(),
+         xbad=X[:, bad[:40]], ybad=Y[:, bad[:40]])
