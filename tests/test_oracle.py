@@ -123,3 +123,43 @@ def test_farmer_ef_golden_fixture_reproduces():
     assert np.allclose([xs[0][i] for i in idx], gold["nonants"], rtol=1e-8)
     # every scenario shares the first stage (non-anticipativity rows)
     assert max(np.max(np.abs(x[idx] - xs[0][idx])) for x in xs) < 1e-7
+
+
+def test_batched_oracle_pins_to_distributed_highs_oracle():
+    """oracle/batch_pdas.py (batched exact active-set prox-QP solves, which
+    generated tests/golden/farmer10k_ph.json) against oracle/ph_dist.py
+    (HiGHS + KKT polish per subproblem on 6 gloo ranks, the `mpiexec -n 6`
+    restatement): same farmer instance, rho 1, convthresh 1e-4, the
+    reference's per-rank convergence metric for 6 ranks
+    (tests/golden/farmer200_ph_dist.json).  The HiGHS path accepts QP points
+    at 1e-9 relative KKT, the batched one is exact to ~1e-14, so values agree
+    to ~1e-8 and the iteration count exactly."""
+    import json
+    import os
+    from oracle.batch_pdas import ph_run
+    with open(os.path.join(os.path.dirname(__file__), "golden", "farmer200_ph_dist.json")) as f:
+        ref = json.load(f)
+    scens = [om.farmer(f"scen{i}", 1) for i in range(ref["S"])]
+    r = ph_run(scens, ref["rho"], ref["convthresh"], 100000, ref["ranks"])
+    assert r["iterations"] == ref["iterations"]
+    assert np.max(np.abs(np.array(r["xbar"]) - ref["xbar"]) / np.abs(ref["xbar"])) < 1e-7
+    assert abs(r["Eobj"] - ref["Eobj"]) < 1e-9 * abs(ref["Eobj"])
+    assert abs(r["trivial_bound"] - ref["trivial_bound"]) < 1e-12 * abs(ref["trivial_bound"])
+    assert abs(float(np.abs(r["W"]).sum()) - ref["W_abs_sum"]) < 1e-7 * ref["W_abs_sum"]
+    for k, w in ref["W_sample"].items():
+        assert np.max(np.abs(r["W"][int(k)] - np.array(w))) < 1e-6 * max(1.0, np.max(np.abs(w)))
+
+
+def test_farmer10k_golden_trajectory_fixture_is_consistent():
+    """tests/golden/farmer10k_ph.json (oracle/batch_pdas.py, 10,000 scenarios,
+    regenerated by `python -m oracle.batch_pdas --scens 10000`, ~25 min):
+    conv below the threshold only at the last pass (the break of
+    phbase.py:1505-1510), xbar within the acreage limit, bound below Eobj."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "farmer10k_ph.json")) as f:
+        g = json.load(f)
+    assert g["S"] == 10000 and g["conv"] < g["convthresh"]
+    assert g["conv_history_tail"][-2] >= g["convthresh"]       # the break is at the first pass below
+    assert 0.0 <= sum(g["xbar"]) <= 500.0 * (1 + 1e-12)          # total acreage (farmer.py:183-186)
+    assert g["trivial_bound"] < g["Eobj"]                       # minimisation: a lower bound
