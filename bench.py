@@ -171,12 +171,33 @@ def _red_dev():
     return "cuda"
 
 
+FP64_VECTOR_PEAK_TFS = 78.6  # MI355X FP64 vector, AMD spec (the microarch guide has no FP64 row)
+
+
+def pdhg_flops_per_step(c):
+    """Algorithmic FP64 flops of one PDHG step of one scenario: SpMV^T and
+    SpMV (2 flops per entry each) + the column update (g - A'y, the prox
+    step, the clip, the reflection and the Halpern average: 10 per column)
+    + the row update (the dual prox, reflection, average: 10 per row)."""
+    n, m, nnz = farmer_dims(c)
+    return 4 * nnz + 10 * n + 10 * m
+
+
 def hbm_config(args, world, farmer, PH, opts):
-    """F3: farmer c=--hbm-crops, --scens scenarios per rank.  Iter0, one
-    warmup iteration, then --hbm-steps PH iterations through the device loop
-    with the library's kernel events; the PDHG kernel's algorithmic bytes are
-    SURVEY 8(d) B_it per scenario-step x the steps taken + every scenario's
-    data in/out."""
+    """F3: farmer c=--hbm-crops, --scens scenarios per rank (the mid-size
+    path: PDHG phase kernels mid_kernel and LDL' polish phases
+    mid_polish_kernel).  Iter0, one warmup
+    iteration, then --hbm-steps PH iterations through the device loop with
+    the library's per-launch HIP events.
+
+    roofline: the solve (all its phase launches) as the unit -- algorithmic
+    bytes = every scenario's data in and solution out (the bytes the solve
+    must move); `traffic` = the PMC-measured HBM bytes of the same phase
+    launches per PH iteration.  `on_chip`: the PDHG phase kernel's FP64 rate
+    (algorithmic flops per PDHG step x steps taken) against the FP64 vector
+    peak.  `streaming_equivalent`: what a PDHG that streamed every step's
+    operands from HBM would need (SURVEY 8(d) B_it) -- a work rate, not a
+    bandwidth measurement."""
     c = args.hbm_crops
     S = args.scens * world
     names = [f"scen{i}" for i in range(S)]
@@ -202,7 +223,7 @@ def hbm_config(args, world, farmer, PH, opts):
     ph.run_device_loop(1, 1 + args.hbm_steps, -1.0, chunk=args.hbm_steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    n_t, as_ms, po_ms, pd_ms = b.read_timing()
+    n_t, as_ms, po_ms, pd_ms, nk, k_ms, np_, p_ms = b.read_timing_full()
     st = b.loop_status()
     b.set_timing(False)
     d = torch.tensor([dt], dtype=torch.float64, device=_red_dev())
@@ -210,24 +231,45 @@ def hbm_config(args, world, farmer, PH, opts):
         dist.all_reduce(d, op=dist.ReduceOp.MAX)
     dt = float(d.item())
     nt = max(n_t, 1)
-    pd_ms /= nt
-    steps_per_launch = st[4] / nt
-    pd_bytes = steps_per_launch * bytes_per_pdhg_iter(c) + ph.S_loc * solve_bytes_per_scenario(c)
-    gbs = pd_bytes / (pd_ms / 1000.0) / 1e9
     n, m, nnz = farmer_dims(c)
+    solve_ms = (k_ms + p_ms) / nt if (nk + np_) else pd_ms / nt   # all phases of one solve
+    steps = st[4] / nt                                                # PDHG steps per solve call
+    alg = ph.S_loc * solve_bytes_per_scenario(c)
+    gbs = alg / (solve_ms / 1000.0) / 1e9
+    stream_bytes = steps * bytes_per_pdhg_iter(c) + alg
+    kern_ms = k_ms / max(nk, 1)
+    tfs = (steps * pdhg_flops_per_step(c)) / (k_ms / nt / 1000.0) / 1e12 if k_ms > 0 else 0.0
+    trf = [pmc_traffic(k, ph.S_loc, c)[0] for k in ("mid_kernel", "mid_polish_kernel")]
+    traffic = None
+    if all(t is not None for t in trf) and nk and np_:
+        traffic = round(trf[0] * nk / nt + trf[1] * np_ / nt)   # HBM bytes per solve call
     return {"workload": f"farmer PH, {S} scenarios ({args.scens} per GPU), crops_multiplier={c} "
                         f"(n={n}, m={m}, nnz={nnz} per scenario), rho={args.rho}",
             "value": round(S * args.hbm_steps / dt, 2), "unit": "solves/s",
             "ms_per_step": round(dt / args.hbm_steps * 1000.0, 3), "steps": args.hbm_steps,
             "iter0_s": round(t_iter0, 3), "iter0_not_optimal": nonopt0,
             "pdhg_steps_per_solve": round(st[4] / max(st[3], 1), 1), "pdhg_steps_max": st[5],
-            "roofline": {"bound": "hbm", "kernel": "pdhg_kernel", "achieved": round(gbs, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "kernel_ms": round(pd_ms, 3), "alg_bytes_per_launch": round(pd_bytes),
-                         "traffic": pmc_traffic("pdhg_kernel", ph.S_loc, c)[0],
-                         "note": "algorithmic = the HBM traffic a streaming PDHG would need "
-                                 "(SURVEY 8(d) B_it per scenario-step); this kernel keeps each "
-                                 "scenario on chip, so frac > 1 is possible"}}
+            "roofline": {"bound": "hbm", "kernel": "mid-size solve (mid_kernel PDHG phases + "
+                                                  "mid_polish_kernel polish phases)",
+                         "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "solve_ms": round(solve_ms, 3), "alg_bytes_per_solve": round(alg),
+                         "launches_per_solve": {"mid_kernel": round(nk / nt, 2),
+                                                "mid_polish_kernel": round(np_ / nt, 2)},
+                         "kernel_ms": {"mid_kernel": round(kern_ms, 4),
+                                       "mid_polish_kernel": round(p_ms / max(np_, 1), 4)},
+                         "note": "algorithmic bytes = each scenario's data in + solution out "
+                                 "(the scenario stays on chip between PDHG steps); traffic = "
+                                 "rocprofv3 PMC bytes of the same phase launches per solve"},
+            "on_chip": {"bound": "fp64-vector", "kernel": "mid_kernel",
+                        "flops_per_step_per_scenario": pdhg_flops_per_step(c),
+                        "achieved": round(tfs, 3), "peak": FP64_VECTOR_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": round(tfs / FP64_VECTOR_PEAK_TFS, 4)},
+            "streaming_equivalent": {"bytes_per_solve": round(stream_bytes),
+                                     "GBps": round(stream_bytes / (solve_ms / 1000.0) / 1e9, 1),
+                                     "note": "SURVEY 8(d) B_it per scenario-step x steps taken: "
+                                             "the bandwidth a PDHG streaming every step's operands "
+                                             "from HBM would need -- a work rate, not a measurement"}}
 
 
 def _spawn_ranks(n, cpu):

@@ -264,12 +264,15 @@ int ph_loop_status(ph_batch_t b, int64_t *out /*host [8]*/);
 /*
  * Kernel timing of ph_pdhg_solve with HIP events recorded on the batch's
  * stream around its kernels of every solve while timing is on (set_timing
- * clears the record).  read_timing synchronises and returns out[4] =
+ * clears the record).  read_timing synchronises and returns out[8] =
  * {solves recorded, total ms of the active-set kernel, of the polish
- * kernel, of the PDHG kernel}.  (Measurement support; bench.py.)
+ * kernel, of the PDHG kernel (one-wave path: from the polish's end to the
+ * solve's end; mid-size path: all phases), launches and total ms of the
+ * mid-size path's PDHG phase kernel, launches and total ms of its polish
+ * phase kernel}.  (Measurement support; bench.py.)
  */
 int ph_batch_set_timing(ph_batch_t b, int32_t on);
-int ph_batch_read_timing(ph_batch_t b, double *out /*host [4]*/);
+int ph_batch_read_timing(ph_batch_t b, double *out /*host [8]*/);
 
 /* Block until all work queued on the batch's stream has finished. */
 int ph_batch_sync(ph_batch_t b);

@@ -338,6 +338,9 @@ struct SolveArgs {
   int32_t *queue;  // work-queue counter (0 at launch)
   // misses polish_kernel could not finish (pdhg_kernel's list when set)
   int32_t *wl2, *wl2_count;
+  // scenarios the solve left short of the tolerance (the rescue polish and
+  // the safe-bound pass take this list), or null
+  int32_t *ul, *ul_count;
   const LoopCtl *ctl;  // device loop control or null
   unsigned long long *prof;  // [16] phase clocks of the warm polish, or null
 };
@@ -1388,6 +1391,7 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     a.diag[PH_DIAG_W * s + 2] = d_eg;
     a.diag[PH_DIAG_W * s + 3] = d_r;
     a.diag[PH_DIAG_W * s + 4] = (double)how;
+    if (stat != PH_STATUS_OPTIMAL && a.ul) a.ul[atomicAdd(a.ul_count, 1)] = s;
   }
   __syncthreads();  // LDS is reused by the block's next scenario
 }
@@ -1611,6 +1615,7 @@ __global__ void loop_conv_kernel(LoopCtl *c, const double *__restrict__ parts,
   ctr[0] = 0;
   ctr[1] = 0;
   ctr[2] = 0;
+  ctr[6] = 0;
 }
 
 // Several ranks, one collective per iteration: the conv partials of pass
@@ -1639,6 +1644,7 @@ __global__ void loop_conv_lagged_kernel(LoopCtl *c, const double *__restrict__ p
     ctr[0] = 0;
     ctr[1] = 0;
     ctr[2] = 0;
+    ctr[6] = 0;
   }
 }
 
@@ -1685,8 +1691,11 @@ __global__ void __launch_bounds__(1024) loop_conv_local_kernel(
     ctr[0] = 0;
     ctr[1] = 0;
     ctr[2] = 0;
+    ctr[6] = 0;
   }
 }
+
+#include "solve_mid.inc"
 
 // ------------------------------------------------------------------------
 // polish_kernel: the misses of the active-set cache (work list wl), one
@@ -2031,14 +2040,26 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
       }
       as = classify_pdas(lane, n, m, XU, LAMU, yn, AXU, L, U, RL, RU);
     }
-    if (!solved && lane == 0) {  // pdhg_kernel: warm polish from the point, then PDHG
+    if (!solved && lane == 0) {  // tail_kernel: warm polish from the point, PDHG, rescue
       a.hint_ok[s] = 0;
       a.wl2[atomicAdd(a.wl2_count, 1)] = s;
     }
   }
 }
 
-#include "solve_mid.inc"
+// The misses the register polish could not finish (wl2), grid-strided over
+// a small grid (the list is short, usually empty): per scenario the
+// one-wave PDHG solve (its warm polish first), then -- short of the
+// tolerance -- the LDL' rescue polish and the safe bound (miss_tail).  One
+// launch for what were pdhg_kernel, the rescue kernel and bound_kernel.
+template <int E>
+__global__ void __launch_bounds__(WAVE) tail_kernel(SolveArgs a, MidArgs md, int has_md) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int count = stopped(a.ctl) ? 0 : *a.wl2_count;
+  for (int idx = blockIdx.x; idx < count; idx += gridDim.x)  // uniform over the block
+    miss_tail<E>(a, has_md ? &md : nullptr, a.wl2[idx], lds);
+}
+
 
 // ------------------------------------------------------------------------
 // nonanticipativity kernels (scenario-fastest, coalesced)
@@ -2278,6 +2299,7 @@ __global__ void __launch_bounds__(POST_BLOCK) update_w_conv_kernel(
     ctr[0] = 0;
     ctr[1] = 0;
     ctr[2] = 0;
+    ctr[6] = 0;
     reset_ticket(ticket);
   }
 }
@@ -2324,7 +2346,8 @@ struct ph_batch {
   int32_t *d_cache_ok = nullptr;
   unsigned long long *d_hint = nullptr;
   int32_t *d_hint_ok = nullptr, *d_wl = nullptr, *d_wl2 = nullptr;
-  int32_t *d_ctr = nullptr;  // [6]: miss list count, pdhg queue, pdhg list count, post ticket, W/conv ticket
+  int32_t *d_ul = nullptr;  // [S] scenarios a solve left short of the tolerance
+  int32_t *d_ctr = nullptr;  // [8]: miss list count, pdhg queue, pdhg list count, post ticket, W/conv ticket, -, unsolved list count
   double *d_sb = nullptr;    // [S][4n+3m] static block (polish-size scenarios)
   LoopCtl *d_ctl = nullptr;  // device loop control
   bool loop_on = false;
@@ -2334,6 +2357,11 @@ struct ph_batch {
   unsigned long long *d_prof = nullptr;  // warm-polish phase clocks (ph_debug_prof)
   std::vector<hipEvent_t> ev;  // 4 per recorded solve: as0, as1 (=pd0), pd1, spare
   size_t ev_used = 0;
+  // mid-size path: an event pair around every phase launch, and its kind
+  // (0: mid_kernel, 1: mid_polish_kernel)
+  std::vector<hipEvent_t> pev;
+  std::vector<int> pkind;
+  size_t pev_used = 0;
   int pdhg_grid = 0;         // resident blocks of the pdhg kernel (0: not yet known)
   double *d_part = nullptr;  // partials of the multi-block reductions
   size_t part_cap = 0;
@@ -2346,6 +2374,7 @@ struct ph_batch {
   // mid-size path (solve_mid): geometry, symbolic KKT analysis, tails
   bool mid = false;        // the mid-size path solves this batch
   bool mid_ready = false;  // its symbolic data is set up (also for the one-wave rescue)
+  bool miss_attr = false;  // tail_kernel's LDS limit raised
   int mblock = 0, mpc = 0, mpr = 0;
   KktSymbolic sym;
   int32_t *d_sym = nullptr;   // every int32 array of the symbolic analysis + tails
@@ -2634,8 +2663,8 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_c, (size_t)S * n)) || (rc = dalloc(&b->d_l, (size_t)S * n)) ||
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
       (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
-      (rc = dalloc(&b->d_summary, 5)) || (rc = dalloc(&b->d_ctr, 6)) || (rc = dalloc(&b->d_ctl, 1)) ||
-      (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
+      (rc = dalloc(&b->d_summary, 5)) || (rc = dalloc(&b->d_ctr, 8)) || (rc = dalloc(&b->d_ctl, 1)) ||
+      (rc = dalloc(&b->d_ul, S)) || (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
     ph_batch_destroy(b);
@@ -2646,7 +2675,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
     ph_batch_destroy(b);
     return fail(PH_EHIP, "ph_batch_create: allocation failed");
   }
-  if (hipMemsetAsync(b->d_ctr, 0, 6 * sizeof(int32_t), b->stream) != hipSuccess) {
+  if (hipMemsetAsync(b->d_ctr, 0, 8 * sizeof(int32_t), b->stream) != hipSuccess) {
     ph_batch_destroy(b);
     return fail(PH_EHIP, "ph_batch_create: clearing counters failed");
   }
@@ -2794,13 +2823,41 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
 
 }  // extern "C"
 
+// Blocks of the list-driven tail kernels (rescue polish, safe bound): the
+// lists are empty in the PH steady state, so a small grid-strided grid.
+constexpr int TAIL_GRID = 512;
+
 // The repaired Lagrangian bound of the scenarios a solve left short of
 // the tolerance (bound_kernel; blocks of the others exit at once).
-static int launch_bound(ph_batch *b, const SolveArgs &a) {
+// list == null: every scenario (grid S); else list[0 .. *count) with a
+// small grid-strided grid.
+static int launch_bound(ph_batch *b, const SolveArgs &a, const int32_t *list, const int32_t *count) {
   if (!b->d_sb) return PH_OK;
   const size_t lds = sizeof(double) * (((size_t)b->n + 1 & ~(size_t)1) + ((size_t)b->m + 1 & ~(size_t)1) + MAX_WAVES);
-  hipLaunchKernelGGL(bound_kernel<256>, dim3(b->S), dim3(256), lds, b->stream, a);
+  const int grid = list ? std::min(b->S, TAIL_GRID) : b->S;
+  hipLaunchKernelGGL(bound_kernel<256>, dim3(grid), dim3(256), lds, b->stream, a, list, count);
   HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+// The one-wave rescue polish runs the <WAVE, 1, 1> instance of the
+// mid-size polish (rescue_kernel, miss_tail).
+static bool one_wave_rescue(const ph_batch *b) {
+  return b->mid_ready && b->mblock == WAVE && b->mpc == 1 && b->mpr == 1;
+}
+
+// Timing of the mid-size path's phase launches: kind >= 0 records the
+// start event of a launch of that kind, kind -1 its end event.
+static int phase_event(ph_batch *b, int kind) {
+  if (!b->timing) return PH_OK;
+  if (b->pev_used + 1 > b->pev.size()) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    b->pev.push_back(e);
+    b->pkind.push_back(0);
+  }
+  b->pkind[b->pev_used] = kind;
+  HIP_OK(hipEventRecord(b->pev[b->pev_used++], b->stream));
   return PH_OK;
 }
 
@@ -2868,22 +2925,24 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   auto pdhg = [&](const int32_t *in, const int32_t *cin, int32_t *out, int32_t *cout, int32_t *q,
                   double exit_err, int first, int hand_at_limit) -> int {
     const MidPhase ph{in, cin, out, cout, q, exit_err, first, 0, hand_at_limit};
+    if (int rc = phase_event(b, 0)) return rc;
     DISPATCH_MID({
       hipLaunchKernelGGL((mid_kernel<B_, C_, R_>), dim3(b->S), dim3(B_), b->mid_lds_bytes,
                          b->stream, a, b->md, ph, b->mid_lds_doubles);
     });
     HIP_OK(hipGetLastError());
-    return PH_OK;
+    return phase_event(b, -1);
   };
   auto polish = [&](const int32_t *in, const int32_t *cin, int32_t *out, int32_t *cout, int32_t *q,
                     int mode) -> int {
     const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode, 0, 0};
+    if (int rc = phase_event(b, 1)) return rc;
     DISPATCH_MID({
       hipLaunchKernelGGL((mid_polish_kernel<B_, C_, R_>), dim3(b->S), dim3(B_),
                          b->mid_plds_bytes, b->stream, a, b->md, ph, b->mid_lds_doubles);
     });
     HIP_OK(hipGetLastError());
-    return PH_OK;
+    return phase_event(b, -1);
   };
   int rc = 0;
   const int32_t *in = nullptr, *cin = nullptr;
@@ -2908,12 +2967,41 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   } else if ((rc = pdhg(in, cin, L[1], C + 1, Q + 1, 0.0, 1, 0))) {
     return rc;
   }
-  if (int rc2 = launch_bound(b, a)) return rc2;
+  // the safe outer bound of every scenario left short of the tolerance
+  // (any phase; blocks of the others exit at once)
+  if ((rc = launch_bound(b, a, nullptr, nullptr))) return rc;
   if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
   const int post_g = (b->loop_on && b->loop_xa.x == a.x) ? b->loop_xa.G : 0;
   hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, a.status,
                      a.iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa);
   HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+// The one-wave path without the active-set cache (Iter0, cold or bound
+// solves): pdhg_kernel over every scenario, then the rescue polish of the
+// ones it left at the iteration limit (its list) and their safe bounds.
+static int cold_tail(ph_batch *b, SolveArgs &a, size_t lds) {
+  DISPATCH_EXT(64, 1, b->ext, {
+    hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(std::min(b->S, b->pdhg_grid)), dim3(B_), lds,
+                       b->stream, a);
+  });
+  HIP_OK(hipGetLastError());
+  if (a.polish && one_wave_rescue(b)) {
+    // rescue: the quasi-definite LDL' polish (regularised, refined: it copes
+    // with the singular active sets of degenerate LPs) from the final PDHG
+    // point of every scenario pdhg_kernel left at the iteration limit (its
+    // list; a small grid, empty in the steady state); a failure gets its
+    // safe outer bound in the same block
+    if (int rc = mid_init(b)) return rc;
+    const MidPhase ph{b->d_ul, b->d_ctr + 6, nullptr, nullptr, nullptr, 0.0, 0, 1, 0, 1};
+    hipLaunchKernelGGL(rescue_kernel, dim3(std::min(b->S, TAIL_GRID)), dim3(WAVE),
+                       std::max(b->mid_plds_bytes, (size_t)8 * (b->n + b->m + 2 + MAX_WAVES)),
+                       b->stream, a, b->md, ph);
+    HIP_OK(hipGetLastError());
+  } else if (int rc = launch_bound(b, a, b->d_ul, b->d_ctr + 6)) {
+    return rc;
+  }
   return PH_OK;
 }
 
@@ -2963,6 +3051,8 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.queue = b->d_ctr + 1;
   a.wl2 = nullptr;
   a.wl2_count = b->d_ctr + 2;
+  a.ul = nullptr;
+  a.ul_count = b->d_ctr + 6;
   a.ctl = loop_ctl(b);
   a.prof = b->d_prof;
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
@@ -2979,7 +3069,11 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     b->pdhg_grid = std::max(1, per_cu) * std::max(1, cus);
   }
   // (in the device loop the convergence kernel has cleared the counters)
-  if (!b->loop_on) HIP_OK(hipMemsetAsync(b->d_ctr, 0, 3 * sizeof(int32_t), b->stream));
+  if (!b->loop_on) {
+    HIP_OK(hipMemsetAsync(b->d_ctr, 0, 3 * sizeof(int32_t), b->stream));
+    HIP_OK(hipMemsetAsync(b->d_ctr + 6, 0, sizeof(int32_t), b->stream));
+  }
+  a.ul = b->d_ul;  // pdhg_kernel lists what it leaves short of the tolerance
   hipEvent_t *tev = nullptr;
   if (b->timing) {
     if (b->ev_used + 4 > b->ev.size()) {
@@ -3025,40 +3119,40 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     }
     HIP_OK(hipGetLastError());
     if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
-    // the misses: register Gauss-Jordan polish; what it cannot finish goes
-    // to pdhg_kernel through the second list
+    // the misses, one wave each: register Gauss-Jordan polish; what it
+    // cannot finish goes to tail_kernel (PDHG, rescue polish, safe bound)
+    a.wl2 = b->d_wl2;
     hipLaunchKernelGGL(polish_kernel, dim3(std::min(b->S, POLISH_GRID)), dim3(WAVE),
                        polish_lds_bytes(b), b->stream, a);
     HIP_OK(hipGetLastError());
-    a.wl = b->d_wl2;
-    a.wl_count = b->d_ctr + 2;
-  }
-  if (tev) {
-    if (!(a.cache && a.warm)) HIP_OK(hipEventRecord(tev[1], b->stream));
-    HIP_OK(hipEventRecord(tev[2], b->stream));
-  }
-  // behind the cache and the polish the PDHG list is short (usually empty):
-  // a small grid drains it from the queue and costs little when empty
-  const int grid = std::min(b->S, (a.cache && a.warm) ? std::min(b->pdhg_grid, 64) : b->pdhg_grid);
-  DISPATCH_EXT(64, 1, b->ext, {
-    hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(grid), dim3(B_), lds, b->stream, a);
-  });
-  HIP_OK(hipGetLastError());
-  if (a.polish && b->mid_ready) {
-    // rescue: the quasi-definite LDL' polish (regularised, refined: it copes
-    // with the singular active sets of degenerate LPs) from the final PDHG
-    // point of every scenario left at the iteration limit; blocks of the
-    // others exit at once
-    if (int rc = mid_init(b)) return rc;
-    const MidPhase ph{nullptr, nullptr, nullptr, nullptr, nullptr, 0.0, 0, 1, 0, 1};
-    DISPATCH_MID({
-      hipLaunchKernelGGL((mid_polish_kernel<B_, C_, R_>), dim3(b->S), dim3(B_), b->mid_plds_bytes,
-                         b->stream, a, b->md, ph, b->mid_lds_doubles);
+    const int has_md = one_wave_rescue(b) ? 1 : 0;
+    if (has_md)
+      if (int rc = mid_init(b)) return rc;
+    size_t tlds = lds;
+    if (has_md) tlds = std::max(tlds, b->mid_plds_bytes);
+    a.ul = nullptr;  // (the tail bounds its failures itself)
+    DISPATCH_EXT(64, 1, b->ext, {
+      if (!b->miss_attr && tlds > 64 * 1024) {
+        HIP_OK(hipFuncSetAttribute((const void *)tail_kernel<E_>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)tlds));
+        b->miss_attr = true;
+      }
+      hipLaunchKernelGGL((tail_kernel<E_>), dim3(std::min(b->S, std::min(b->pdhg_grid, 64))),
+                         dim3(WAVE), tlds, b->stream, a, b->md, has_md);
     });
     HIP_OK(hipGetLastError());
+    if (tev) {
+      HIP_OK(hipEventRecord(tev[2], b->stream));
+      HIP_OK(hipEventRecord(tev[3], b->stream));
+    }
+  } else {
+    if (tev) {
+      HIP_OK(hipEventRecord(tev[1], b->stream));
+      HIP_OK(hipEventRecord(tev[2], b->stream));
+    }
+    if (int rc = cold_tail(b, a, lds)) return rc;
+    if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
   }
-  if (int rc = launch_bound(b, a)) return rc;
-  if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
   // device loop: the summary block also advances the iteration, and G
   // more blocks compute the next iteration's Compute_Xbar sums
   const int post_g = (b->loop_on && b->loop_xa.x == x) ? b->loop_xa.G : 0;
@@ -3067,6 +3161,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
+
 
 int ph_xbar_accum(ph_batch_t b, const double *x, const double *prob_coeff, int32_t G,
                   const int32_t *slot_k, const int32_t *slot_s0, const int32_t *slot_s1,
@@ -3246,6 +3341,7 @@ int ph_batch_set_timing(ph_batch_t b, int32_t on) {
   if (!b) return fail(PH_EINVAL, "null batch");
   b->timing = on != 0;
   b->ev_used = 0;
+  b->pev_used = 0;
   return PH_OK;
 }
 
@@ -3264,6 +3360,15 @@ int ph_batch_read_timing(ph_batch_t b, double *out) {
   out[1] = t[0];
   out[2] = t[1];
   out[3] = t[2];
+  // mid-size phases: launches and total ms of mid_kernel, of mid_polish_kernel
+  out[4] = out[5] = out[6] = out[7] = 0.0;
+  for (size_t i = 0; i + 1 < b->pev_used; i += 2) {
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, b->pev[i], b->pev[i + 1]));
+    const int k = b->pkind[i] == 1 ? 1 : 0;
+    out[4 + 2 * k] += 1.0;
+    out[5 + 2 * k] += ms;
+  }
   return PH_OK;
 }
 
@@ -3302,12 +3407,13 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
-                  b->d_sb, b->d_part,
+                  b->d_ul, b->d_sb, b->d_part,
                   b->d_ctl, b->d_sym, b->d_ws, b->d_mlist, b->d_mctr,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : b->ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : b->pev) (void)hipEventDestroy(e);
   delete b;
 }
 

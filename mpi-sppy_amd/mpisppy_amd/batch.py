@@ -228,10 +228,16 @@ class DeviceBatch:
 
     def read_timing(self):
         """(solves, total ms of the active-set, polish and PDHG kernels); syncs."""
-        out = np.zeros(4)
+        return self.read_timing_full()[:4]
+
+    def read_timing_full(self):
+        """read_timing + (launches, total ms) of the mid-size path's PDHG phase
+        kernel and of its polish phase kernel; syncs."""
+        out = np.zeros(8)
         _native.check(self.lib.ph_batch_read_timing(self.handle, out.ctypes.data_as(_native._c_ptr)),
                       "ph_batch_read_timing")
-        return int(out[0]), float(out[1]), float(out[2]), float(out[3])
+        return (int(out[0]), float(out[1]), float(out[2]), float(out[3]),
+                int(out[4]), float(out[5]), int(out[6]), float(out[7]))
 
     def kernel_ms_all(self):
         """Durations (ms) of every solve recorded in event_log (synchronises)."""
