@@ -259,6 +259,14 @@ int ph_loop_conv_lagged(ph_batch_t b, const double *parts /*dev [R]*/,
                         double *conv_hist /*dev [iter_limit]*/);
 int ph_loop_backup(ph_batch_t b, const double *x, double *x_save, int64_t nx,
                    const double *y, double *y_save, int64_t ny);
+/*
+ * With ph_loop_backup: the solve's status [S] and outer bound [S] saved
+ * under the same stop check, so a convergence break restores the
+ * reference's statuses and bounds too (phbase.py:1505-1510 breaks before
+ * the solve; scenario_feasible and Ebound then describe the last solve run).
+ */
+int ph_loop_backup_status(ph_batch_t b, const int32_t *status, int32_t *status_save,
+                          const double *dbound, double *dbound_save);
 int ph_loop_status(ph_batch_t b, int64_t *out /*host [8]*/);
 
 /*

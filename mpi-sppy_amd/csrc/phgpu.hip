@@ -1662,6 +1662,20 @@ __global__ void __launch_bounds__(256) loop_backup_kernel(LoopCtl *c, const doub
   if (blockIdx.x == 0 && threadIdx.x == 0) c->pend = c->iter;
 }
 
+// The solve's per-scenario status and outer bound, saved with x/y (same
+// stop check): a convergence break restores the reference's state -- the
+// last solve the reference ran -- for scenario_feasible and Ebound.
+__global__ void __launch_bounds__(256) loop_backup_status_kernel(
+    const LoopCtl *c, const int32_t *__restrict__ st, int32_t *__restrict__ stb,
+    const double *__restrict__ db, double *__restrict__ dbb, int S) {
+  if (stopped(c)) return;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < S) {
+    stb[s] = st[s];
+    dbb[s] = db[s];
+  }
+}
+
 // Single-rank form: the per-reference-rank sums of absdiff over the
 // segments and the conv test in one block (deterministic order).
 __global__ void __launch_bounds__(1024) loop_conv_local_kernel(
@@ -3386,6 +3400,16 @@ int ph_loop_backup(ph_batch_t b, const double *x, double *x_save, int64_t nx, co
   const int grid = (int)std::min<long>(std::max<long>((mx + 255) / 256, 1), 2048);
   hipLaunchKernelGGL(loop_backup_kernel, dim3(grid), dim3(256), 0, b->stream, b->d_ctl, x, x_save,
                      (long)nx, y, y_save, (long)ny);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_loop_backup_status(ph_batch_t b, const int32_t *status, int32_t *status_save,
+                          const double *dbound, double *dbound_save) {
+  if (!b || !b->loop_on || !status || !status_save || !dbound || !dbound_save)
+    return fail(PH_EINVAL, "ph_loop_backup_status: bad arguments (or loop not enabled)");
+  hipLaunchKernelGGL(loop_backup_status_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream,
+                     b->d_ctl, status, status_save, dbound, dbound_save, b->S);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }

@@ -60,6 +60,7 @@ SIGNATURES = [
     ("ph_loop_conv_lagged", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_int, _c_dbl, _c_ptr]),
     ("ph_loop_backup", _c_int, [_c_ptr, _c_ptr, _c_ptr, ctypes.c_int64, _c_ptr, _c_ptr,
                                 ctypes.c_int64]),
+    ("ph_loop_backup_status", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
     ("ph_loop_status", _c_int, [_c_ptr, _c_ptr]),
     ("ph_batch_set_timing", _c_int, [_c_ptr, _c_int]),
     ("ph_batch_read_timing", _c_int, [_c_ptr, _c_ptr]),

@@ -313,6 +313,14 @@ class DeviceBatch:
                                               _native.ptr(y_save), self.y.numel()),
                       "ph_loop_backup")
 
+    def loop_backup_status(self, status_save, dbound_save):
+        """Save the solve's status and outer bound with x/y (same stop check)."""
+        _native.check(self.lib.ph_loop_backup_status(self.handle, _native.ptr(self.status),
+                                                     _native.ptr(status_save),
+                                                     _native.ptr(self.dbound),
+                                                     _native.ptr(dbound_save)),
+                      "ph_loop_backup_status")
+
     def loop_status(self):
         """(stop, iter, not-optimal solves, solves, PDHG iters sum, max, polished,
         cached); synchronises.  stop: 0 running, 1 converged, 2 iteration limit."""

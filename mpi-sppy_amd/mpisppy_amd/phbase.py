@@ -549,7 +549,10 @@ class PHBase(SPBase):
             if self._x_save is None:
                 self._x_save = torch.empty_like(b.x)
                 self._y_save = torch.empty_like(b.y)
+                self._st_save = torch.empty_like(b.status)
+                self._db_save = torch.empty_like(b.dbound)
             b.loop_backup(self._x_save, self._y_save)
+            b.loop_backup_status(self._st_save, self._db_save)
         b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
 
     def run_device_loop(self, start_iter, iter_limit, convthresh, chunk=None):
@@ -610,8 +613,15 @@ class PHBase(SPBase):
                 stop, it = st[0], st[1]
                 nonopt = nonopt or st[2]
                 if stop == 1 and self._x_save is not None:
+                    # the reference's state at its break: x/y, statuses and
+                    # outer bounds of the last solve it ran (the cached
+                    # active-set maps stay valid: they depend on the active
+                    # set, not on the point)
                     b.x.copy_(self._x_save)
                     b.y.copy_(self._y_save)
+                    b.status.copy_(self._st_save)
+                    b.dbound.copy_(self._db_save)
+                    nonopt = int((b.status != 0).sum().item())
         finally:
             b.loop_enable(False)
             b.loop_set_xbar(None, None, None, None, None)

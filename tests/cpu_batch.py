@@ -112,6 +112,12 @@ class CPUBatch:
         y_save.copy_(self.y)
         self._ctl["pend"] = self._ctl["iter"]
 
+    def loop_backup_status(self, status_save, dbound_save):
+        if self._stopped():
+            return
+        status_save.copy_(self.status)
+        dbound_save.copy_(self.dbound)
+
     def loop_status(self):
         c = self._ctl
         return (c["stop"], c["iter"], *c["acc"])
