@@ -164,6 +164,11 @@ def pmc_traffic(kname, S_loc, c):
     return None, None
 
 
+def _progress(msg):
+    """A progress line on stderr (long profiled runs must keep writing)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _red_dev():
     """Device of the timing max-reductions: the GPU under RCCL, host under gloo."""
     if dist.is_initialized() and dist.get_backend() == "gloo":
@@ -208,6 +213,7 @@ def hbm_config(args, world, farmer, PH, opts):
     ph._create_solvers()
     b = ph.batch
     torch.cuda.synchronize()
+    _progress("F3 Iter0")
     t0 = time.perf_counter()
     ph.Iter0()
     torch.cuda.synchronize()
@@ -407,11 +413,14 @@ def run():
             "defaultPHrho": args.rho, "convthresh": -1.0, "verbose": False,
             "display_progress": False, "display_timing": False,
             "iter0_solver_options": {}, "iterk_solver_options": {}}
+    _progress(f"building {S} scenarios (crops_multiplier {c})")
     ph = PH(opts, names, farmer.scenario_creator,
             scenario_creator_kwargs={"crops_multiplier": c})
     ph.PH_Prep()
     ph.subproblem_creation()
+    _progress("Iter0")
     ph.Iter0()
+    _progress("warmup + timed PH iterations")
 
     # iterk_loop passes (phbase.py:1498-1553: Compute_Xbar -> Update_W ->
     # convergence_diff -> solve) queued on the device and replayed as one
@@ -516,7 +525,9 @@ def run():
                 "trivial_bound": tb, "Eobj": eobj, "scenarios": S_tol, "n_gpus": world}
 
     tol_info = tol_small = None
+    _progress("timed region done")
     if args.tol_run:
+        _progress("PH to tolerance")
         tol_info = ph_to_tol(args.tol_scens)
         if args.cpu_scens != args.tol_scens:
             tol_small = ph_to_tol(args.cpu_scens)
@@ -525,6 +536,7 @@ def run():
     # 100, 10k scenarios per GPU -- the PDHG kernel's regime
     f3 = None
     if args.hbm_crops > 0:
+        _progress("companion config F3")
         f3 = hbm_config(args, world, farmer, PH, opts)
 
 

@@ -9,20 +9,46 @@ spokes) or nonant values (to nonant spokes) followed by the spoke's batched
 solve; the bounds come back through the spokes' own allreduces.  The hub's
 gap bookkeeping and termination test follow ``hub.py:60-137`` and
 ``PHHub.is_converged`` (``hub.py:430-466``).  Syncs happen every
-``sync_every`` PH iterations (the reference's spokes are asynchronous and
-report whenever they finish).
+``sync_every`` PH iterations.
+
+Asynchronous spokes (``async_spokes``, default on): each spoke's batch runs
+on its own HIP stream.  At a sync the hub first harvests what every spoke
+launched at the previous sync (waiting only if it is still running), then
+launches new work at its current W / nonants -- a device-to-device copy the
+hub's stream waits for, then the spoke's solves, which overlap the hub's next
+PH iterations on the GPU.  A spoke's bound therefore describes the hub's
+state one sync earlier, as a reference spoke's bound describes the W it last
+read from its window (``spoke.py:59-111``); the schedule is the same on
+every rank, so the spokes' collectives stay matched.  ``hub_finalize``
+harvests and then runs one blocking sync at the final state.
 """
+import contextlib
 import math
+
+import torch
 
 from .. import global_toc
 
 
+def spoke_stream(opt):
+    """Context: torch's current stream becomes the spoke batch's own stream,
+    ordered after the caller's current stream (no-op for CPU batches or a
+    batch on the default stream)."""
+    b = getattr(opt, "batch", None)
+    ts = getattr(b, "stream", None) if b is not None else None
+    if not isinstance(ts, torch.cuda.Stream):
+        return contextlib.nullcontext()
+    ts.wait_stream(torch.cuda.current_stream(ts.device))
+    return torch.cuda.stream(ts)
+
+
 class PHHub:
-    def __init__(self, opt, spokes=(), options=None, sync_every=1):
+    def __init__(self, opt, spokes=(), options=None, sync_every=1, async_spokes=True):
         self.opt = opt
         self.spokes = list(spokes)
         self.options = dict(options or {})
         self.sync_every = max(1, int(sync_every))
+        self.async_spokes = bool(async_spokes)
         self.global_rank = opt.cylinder_rank
         self.print_init = True
         self.latest_ib_char = None
@@ -116,11 +142,18 @@ class PHHub:
             return
         self._last_sync = self.opt._PHIter
         for sp in self.spokes:
-            b = sp.hub_sync(self.opt)
-            if sp.bound_kind == "outer":
-                self.OuterBoundUpdate(b, sp.converger_spoke_char)
+            if self.async_spokes and hasattr(sp, "launch"):
+                if getattr(sp, "in_flight", False):
+                    self._update(sp, sp.harvest())
+                sp.launch(self.opt)
             else:
-                self.InnerBoundUpdate(b, sp.converger_spoke_char)
+                self._update(sp, sp.hub_sync(self.opt))
+
+    def _update(self, sp, b):
+        if sp.bound_kind == "outer":
+            self.OuterBoundUpdate(b, sp.converger_spoke_char)
+        else:
+            self.InnerBoundUpdate(b, sp.converger_spoke_char)
 
     def sync_with_spokes(self):
         self.sync()
@@ -145,10 +178,9 @@ class PHHub:
         return self.opt.ph_main()
 
     def hub_finalize(self):
-        """Final bounds from the spokes at the hub's last W / nonants."""
+        """Final bounds from the spokes at the hub's last W / nonants (what is
+        still in flight first)."""
         for sp in self.spokes:
-            b = sp.hub_sync(self.opt)
-            if sp.bound_kind == "outer":
-                self.OuterBoundUpdate(b, sp.converger_spoke_char)
-            else:
-                self.InnerBoundUpdate(b, sp.converger_spoke_char)
+            if getattr(sp, "in_flight", False):
+                self._update(sp, sp.harvest())
+            self._update(sp, sp.hub_sync(self.opt))

@@ -62,13 +62,24 @@ class XhatBase:
 
     def _try_one(self, snamedict, solver_options=None, verbose=False, restore_nonants=True):
         """xhatbase.py:35-145: expected objective at the candidate, or None."""
+        kw = self._try_one_launch(snamedict, solver_options)
+        return self._try_one_finish(kw, verbose, restore_nonants)
+
+    def _try_one_launch(self, snamedict, solver_options=None):
+        """The candidate's nonants fixed and the batched solve queued (not
+        waited for; asynchronous spokes).  Returns the solve keywords."""
         opt = self.opt
         xg = self._xhat_from(snamedict)
         opt._save_nonants()
         opt._fix_nonants(xg)
         sopt = dict(solver_options or {})
         sopt.setdefault("pdhg_max_iters", int(opt.options.get("xhat_max_iters", 50000)))
-        opt.solve_loop(solver_options=sopt, dis_W=True, dis_prox=True, verbose=verbose)
+        return opt.solve_loop_launch(solver_options=sopt, dis_W=True, dis_prox=True)
+
+    def _try_one_finish(self, kw, verbose=False, restore_nonants=True):
+        """Wait for the candidate's solve; E[objective] or None."""
+        opt = self.opt
+        opt.solve_loop_finish(kw)
         status = opt.batch.status.cpu().numpy()
         solved = opt.comm.allreduce_host([float(np.sum(status != 0))])[0] == 0.0
         if not solved or opt.infeas_prob() != 0.0:

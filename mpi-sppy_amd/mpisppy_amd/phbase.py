@@ -237,10 +237,49 @@ class PHBase(SPBase):
             return
         from .batch import DeviceBatch
         t0 = time.time()
-        self.batch = DeviceBatch(self.batch_data, device=self.device)
+        stream = None
+        if getattr(self, "_own_stream", False) and self.device.type == "cuda":
+            # a spoke's batch: its kernels on a stream of their own, so they
+            # overlap the hub's (cylinders/hub.py, asynchronous spokes)
+            stream = torch.cuda.Stream(self.device)
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+        self.batch = DeviceBatch(self.batch_data, device=self.device, stream=stream)
         self.set_instance_time = time.time() - t0
 
     # ----------------------------------------------------------- solves --
+    def solve_loop_launch(self, solver_options=None, dis_W=False, dis_prox=False):
+        """The device half of solve_loop: the batched solve is queued on the
+        batch's stream and not waited for (asynchronous spokes).  Returns the
+        solve keywords for solve_loop_finish."""
+        if dis_W and dis_prox:
+            self._disable_W_and_prox()
+        elif dis_W:
+            self._disable_W()
+        elif dis_prox:
+            self._disable_prox()
+        if self.batch is None:
+            self._create_solvers()
+        kw = self._solve_kwargs(solver_options)
+        self._launch_t0 = time.perf_counter()
+        self.batch.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
+        # (the flags were read at launch)
+        if dis_W and dis_prox:
+            self._reenable_W_and_prox()
+        elif dis_W:
+            self._reenable_W()
+        elif dis_prox:
+            self._reenable_prox()
+        return kw
+
+    def solve_loop_finish(self, kw, gripe=False):
+        """The host half of solve_loop: wait for the solve, statuses ->
+        scenario_feasible (phbase.py:959-989)."""
+        nonopt, it_sum, it_max, npol, ncache = self.batch.summary()  # waits for the solve
+        dt = time.perf_counter() - self._launch_t0
+        self.solve_log.append((self.S_loc, dt, it_sum / max(self.S_loc, 1), it_max,
+                               npol + ncache))
+        self._set_feasibility(nonopt, gripe, kw["max_iters"])
+
     def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False,
                    dtiming=False, dis_W=False, dis_prox=False, gripe=False,
                    disable_pyomo_signal_handling=False, tee=False, verbose=False):

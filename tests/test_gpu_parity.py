@@ -206,11 +206,14 @@ def test_xhat_inner_bounds_match_oracle():
         assert abs(obj - ref) / abs(ref) < 1e-7, (obj, ref)
 
 
-def test_spin_the_wheel_hub_lagrangian_xhat():
+@pytest.mark.parametrize("async_spokes", [True, False])
+def test_spin_the_wheel_hub_lagrangian_xhat(async_spokes):
     """utils.sputils.spin_the_wheel with the reference's dict structure
     (examples/farmer/farmer_cylinders.py): PH hub + Lagrangian outer-bound
     spoke + xhat shuffle inner-bound spoke on the GPU; the bounds bracket
-    the EF optimum and the hub stops on the relative gap."""
+    the EF optimum and the hub stops on the relative gap.  async: the
+    spokes' solves run on their own streams, overlapping the hub's
+    iterations (cylinders/hub.py)."""
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.phbase import PHBase
     from mpisppy_amd.cylinders.hub import PHHub
@@ -221,7 +224,8 @@ def test_spin_the_wheel_hub_lagrangian_xhat():
     from oracle.ef import solve_ef
     names = [f"scen{i}" for i in range(30)]
     base = dict(scenario_creator=farmer.scenario_creator, all_scenario_names=names)
-    hub_dict = {"hub_class": PHHub, "hub_kwargs": {"options": {"rel_gap": 0.002}, "sync_every": 5},
+    hub_dict = {"hub_class": PHHub, "hub_kwargs": {"options": {"rel_gap": 0.002}, "sync_every": 5,
+                                                   "async_spokes": async_spokes},
                 "opt_class": PH,
                 "opt_kwargs": dict(PHoptions=_opts(PHIterLimit=500, convthresh=-1.0), **base)}
     spokes = [{"spoke_class": LagrangianOuterBound, "opt_class": PHBase,
@@ -234,6 +238,8 @@ def test_spin_the_wheel_hub_lagrangian_xhat():
     assert hub.BestInnerBound >= ef * (1 + 1e-7)
     assert hub.compute_gap() <= 0.002
     assert hub.opt._PHIter < 500
+    if async_spokes:  # the spokes' batches ran on streams of their own
+        assert all(sp.opt.batch.stream is not None for sp in hub.spokes)
 
 
 def test_farmer_10k_ph_converges_to_extensive_form():
