@@ -2083,6 +2083,12 @@ struct XbarArgs {  // Compute_Xbar's weighted sums (see ph_xbar_accum)
   const double *x, *pc;
   const int32_t *nonant_col, *slot_k, *s0, *s1;
   double *out;  // [2G]
+  // the post-solve kernel splits each slot's scenario range into C chunks
+  // (one block each; partials [G][C][2], combined in chunk order by the
+  // block that takes the last ticket)
+  int C;
+  double *part;
+  int32_t *ticket;
 };
 
 __device__ __forceinline__ void xbar_sums_block(const XbarArgs &xa, int g) {
@@ -2110,6 +2116,31 @@ __device__ __forceinline__ void xbar_sums_block(const XbarArgs &xa, int g) {
   if (threadIdx.x == 0) {
     xa.out[g] = v[0];
     xa.out[xa.G + g] = v[1];
+  }
+}
+
+// One chunk (c of xa.C) of slot g's scenario range: (sum p x, sum p x^2).
+__device__ __forceinline__ void xbar_chunk(const XbarArgs &xa, int g, int c, double v[2]) {
+  const int k = xa.slot_k[g];
+  const double *xr = xa.x + (size_t)xa.nonant_col[k] * xa.S;
+  const double *pr = xa.pc + (size_t)k * xa.S;
+  const int r0 = xa.s0[g], len = xa.s1[g] - r0;
+  const int c0 = r0 + (int)((long)len * c / xa.C), c1 = r0 + (int)((long)len * (c + 1) / xa.C);
+  v[0] = v[1] = 0.0;
+  const int bd = blockDim.x;
+  for (int s0 = c0 + threadIdx.x; s0 < c1; s0 += 2 * bd) {
+    double xv[2], p[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int s = s0 + u * bd;
+      xv[u] = s < c1 ? xr[s] : 0.0;
+      p[u] = s < c1 ? pr[s] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      v[0] += p[u] * xv[u];
+      v[1] += p[u] * xv[u] * xv[u];
+    }
   }
 }
 
@@ -2190,34 +2221,83 @@ __device__ __forceinline__ void reset_ticket(int32_t *ticket) {
 }
 
 constexpr int POST_BLOCK = 256;
+constexpr int SUM_CHUNK = 2048;  // scenarios per post-solve Compute_Xbar block (2 loads / thread)
 constexpr int POST_COMB = 2048;  // LDS doubles of a combine chunk
 
 // Block 0: (not optimal, sum iters, max iters, polished, cached) of the last
-// solve (polished: how 1/2, cached: how 3).
+// solve (polished: how 1/2, cached: how 3).  After a cached solve (ctr !=
+// null) only the tail list wl2[0 .. ctr[2]) can hold PDHG iterations or a
+// failure: every other scenario was a cache hit (S - ctr[0] of them) or
+// finished by the register polish (ctr[0] - ctr[2]), so block 0 scans the
+// short list instead of all S.
+// Blocks 1 .. G*C (device loop): the next iteration's Compute_Xbar sums in
+// chunks, combined by the last block (XbarArgs).
 // A reduction instead of per-workgroup atomics on one address, which
 // serialise 10k+ workgroups at the end of the solve.
 __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__restrict__ status,
                                                        const int32_t *__restrict__ iters,
                                                        const double *__restrict__ diag,
                                                        unsigned long long *__restrict__ out,
-                                                       LoopCtl *ctl, XbarArgs xa) {
+                                                       LoopCtl *ctl, XbarArgs xa,
+                                                       const int32_t *__restrict__ ctr,
+                                                       const int32_t *__restrict__ wl2) {
   __shared__ unsigned long long red[5][MAX_WAVES];
   if (stopped(ctl)) return;
-  if (blockIdx.x > 0) {  // device loop: next iteration's Compute_Xbar sums
+  if (blockIdx.x > 0 && xa.C == 0) {  // device loop, one block per node slot
     xbar_sums_block(xa, blockIdx.x - 1);
+    return;
+  }
+  if (blockIdx.x > 0) {  // device loop: next iteration's Compute_Xbar sums in chunks
+    __shared__ double xr[2 * MAX_WAVES];
+    const int b = blockIdx.x - 1, g = b / xa.C, c = b % xa.C;
+    double v[2];
+    xbar_chunk(xa, g, c, v);
+    block_sum<2>(v, xr);
+    if (threadIdx.x == 0) {
+      pub(xa.part + 2 * (size_t)b, v[0]);
+      pub(xa.part + 2 * (size_t)b + 1, v[1]);
+    }
+    // (the ticket counts the G*C chunk blocks only)
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      last = __hip_atomic_fetch_add(xa.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             xa.G * xa.C - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    for (int gg = threadIdx.x; gg < xa.G; gg += blockDim.x) {
+      double a0 = 0.0, a1 = 0.0;
+      for (int cc = 0; cc < xa.C; ++cc) {  // chunk order: deterministic
+        a0 += sub(xa.part + 2 * ((size_t)gg * xa.C + cc));
+        a1 += sub(xa.part + 2 * ((size_t)gg * xa.C + cc) + 1);
+      }
+      xa.out[gg] = a0;
+      xa.out[xa.G + gg] = a1;
+    }
+    if (threadIdx.x == 0) {
+      reset_ticket(xa.ticket);
+      // the iteration advances here, after every chunk block has passed its
+      // stop check (block 0 advancing could stop blocks that have not
+      // started, and their tickets would be missing)
+      if (ctl) loop_advance(ctl);
+    }
     return;
   }
   unsigned long long v[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
   const int bd = blockDim.x;
-  for (int s0 = threadIdx.x; s0 < S; s0 += 4 * bd) {
+  const int nl = ctr ? ctr[2] : S;  // scenarios to scan
+  for (int s0 = threadIdx.x; s0 < nl; s0 += 4 * bd) {
     int st[4], itr[4];
     double hw[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {  // independent loads in flight
-      const int s = s0 + u * bd;
-      st[u] = s < S ? status[s] : PH_STATUS_OPTIMAL;
-      itr[u] = s < S ? iters[s] : 0;
-      hw[u] = s < S ? diag[PH_DIAG_W * (size_t)s + 4] : 0.0;
+      const int q = s0 + u * bd;
+      const int s = q < nl ? (ctr ? wl2[q] : q) : 0;
+      st[u] = q < nl ? status[s] : PH_STATUS_OPTIMAL;
+      itr[u] = q < nl ? iters[s] : 0;
+      hw[u] = q < nl ? diag[PH_DIAG_W * (size_t)s + 4] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -2248,6 +2328,10 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
       for (int w = 1; w < nw; ++w) t = i == 2 ? (red[i][w] > t ? red[i][w] : t) : t + red[i][w];
       out[i] = t;
     }
+    if (ctr) {  // the scenarios the cache and the register polish finished
+      out[3] += (unsigned long long)(ctr[0] - ctr[2]);
+      out[4] += (unsigned long long)(S - ctr[0]);
+    }
     if (ctl) {  // running totals of the device loop, then the next iteration
       ctl->acc[0] += out[0];
       ctl->acc[1] += (unsigned long long)S;
@@ -2255,7 +2339,7 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
       ctl->acc[3] = out[2] > ctl->acc[3] ? out[2] : ctl->acc[3];
       ctl->acc[4] += out[3];
       ctl->acc[5] += out[4];
-      loop_advance(ctl);
+      if (gridDim.x == 1 || xa.C == 0) loop_advance(ctl);  // else the last chunk block advances
     }
   }
 }
@@ -2361,6 +2445,8 @@ struct ph_batch {
   unsigned long long *d_hint = nullptr;
   int32_t *d_hint_ok = nullptr, *d_wl = nullptr, *d_wl2 = nullptr;
   int32_t *d_ul = nullptr;  // [S] scenarios a solve left short of the tolerance
+  double *d_xpart = nullptr;  // post-solve Compute_Xbar chunk partials [G][C][2]
+  size_t xpart_cap = 0;
   int32_t *d_ctr = nullptr;  // [8]: miss list count, pdhg queue, pdhg list count, post ticket, W/conv ticket, -, unsolved list count
   double *d_sb = nullptr;    // [S][4n+3m] static block (polish-size scenarios)
   LoopCtl *d_ctl = nullptr;  // device loop control
@@ -2475,6 +2561,19 @@ void build_chunks(int lines, const std::vector<int32_t> &ptr, std::vector<int32_
 // and PR rows per thread (instances listed in DISPATCH_MID).
 bool pick_mid(int n, int m, int *blk, int *pc, int *pr) {
   const int mx = n > m ? n : m;
+  {  // PHGPU_MID_GEOM=512: 512-thread blocks with up to 3 lines per thread
+     // (measurement hook: 1024-thread blocks are capped at 128 VGPRs and spill)
+    static const int g = [] {
+      const char *e = std::getenv("PHGPU_MID_GEOM");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (g == 512 && mx > 512 && n <= 1536 && m <= 1536) {
+      *blk = 512;
+      *pc = (n + 511) / 512;
+      *pr = (m + 511) / 512;
+      if (*pc == 3 && *pr == 2) return true;
+    }
+  }
   for (int B : {64, 128, 256, 512})
     if (mx <= B) {
       *blk = B;
@@ -2503,7 +2602,7 @@ bool pick_mid(int n, int m, int *blk, int *pc, int *pr) {
     MID_CASE(1024, 1, 2, __VA_ARGS__) MID_CASE(1024, 2, 2, __VA_ARGS__)            \
     MID_CASE(1024, 3, 1, __VA_ARGS__) MID_CASE(1024, 3, 2, __VA_ARGS__)            \
     MID_CASE(1024, 1, 3, __VA_ARGS__) MID_CASE(1024, 2, 3, __VA_ARGS__)            \
-    MID_CASE(1024, 3, 3, __VA_ARGS__)                                              \
+    MID_CASE(1024, 3, 3, __VA_ARGS__) MID_CASE(512, 3, 2, __VA_ARGS__)             \
     else return fail(PH_EINVAL, "internal: no mid-size kernel instance");          \
   } while (0)
 
@@ -2988,9 +3087,10 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   // (any phase; blocks of the others exit at once)
   if ((rc = launch_bound(b, a, nullptr, nullptr))) return rc;
   if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
-  const int post_g = (b->loop_on && b->loop_xa.x == a.x) ? b->loop_xa.G : 0;
+  const int post_g = (b->loop_on && b->loop_xa.x == a.x) ? b->loop_xa.G * std::max(1, b->loop_xa.C) : 0;
   hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, a.status,
-                     a.iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa);
+                     a.iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa,
+                     (const int32_t *)nullptr, (const int32_t *)nullptr);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -3172,9 +3272,12 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   }
   // device loop: the summary block also advances the iteration, and G
   // more blocks compute the next iteration's Compute_Xbar sums
-  const int post_g = (b->loop_on && b->loop_xa.x == x) ? b->loop_xa.G : 0;
+  const int post_g = (b->loop_on && b->loop_xa.x == x) ? b->loop_xa.G * std::max(1, b->loop_xa.C) : 0;
+  const bool cached = a.cache && a.warm;  // block 0 scans only the tail list
   hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, status,
-                     iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa);
+                     iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa,
+                     cached ? (const int32_t *)b->d_ctr : nullptr,
+                     cached ? (const int32_t *)b->d_wl2 : nullptr);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -3186,7 +3289,8 @@ int ph_xbar_accum(ph_batch_t b, const double *x, const double *prob_coeff, int32
   if (!b || !x || !prob_coeff || G <= 0 || !slot_k || !slot_s0 || !slot_s1 || !out_sums)
     return fail(PH_EINVAL, "ph_xbar_accum: bad arguments");
   if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_xbar_accum: no nonants declared");
-  const XbarArgs xa{b->S, G, x, prob_coeff, b->d_nonant_col, slot_k, slot_s0, slot_s1, out_sums};
+  const XbarArgs xa{b->S, G, x, prob_coeff, b->d_nonant_col, slot_k, slot_s0, slot_s1, out_sums,
+                    1, nullptr, nullptr};
   hipLaunchKernelGGL(xbar_accum_kernel, dim3(G), dim3(1024), 0, b->stream, xa, loop_ctl(b));
   HIP_OK(hipGetLastError());
   return PH_OK;
@@ -3271,7 +3375,24 @@ int ph_loop_set_xbar(ph_batch_t b, const double *x, const double *prob_coeff, in
   }
   if (!x || !prob_coeff || !slot_k || !slot_s0 || !slot_s1 || !out_sums || !b->d_nonant_col)
     return fail(PH_EINVAL, "ph_loop_set_xbar: bad arguments");
-  b->loop_xa = XbarArgs{b->S, G, x, prob_coeff, b->d_nonant_col, slot_k, slot_s0, slot_s1, out_sums};
+  if (b->mid) {  // one block per node slot (the chunked
+                 // form faulted on this path's graph replays)
+    b->loop_xa = XbarArgs{b->S, G, x, prob_coeff, b->d_nonant_col, slot_k, slot_s0, slot_s1, out_sums,
+                          0, nullptr, nullptr};
+    return PH_OK;
+  }
+  // chunks of at most SUM_CHUNK scenarios per slot, their partials, a ticket
+  const int C = std::max(1, (b->S + SUM_CHUNK - 1) / SUM_CHUNK);
+  if ((size_t)2 * G * C > b->xpart_cap) {
+    if (b->d_xpart) HIP_OK(hipFree(b->d_xpart));
+    b->d_xpart = nullptr;
+    b->xpart_cap = 0;
+    if (int rc = dalloc(&b->d_xpart, (size_t)2 * G * C)) return rc;
+    b->xpart_cap = (size_t)2 * G * C;
+  }
+  b->loop_xa = XbarArgs{b->S, G, x, prob_coeff, b->d_nonant_col, slot_k, slot_s0, slot_s1, out_sums,
+                        C, b->d_xpart, b->d_ctr + 5};
+  HIP_OK(hipMemsetAsync(b->d_ctr + 5, 0, sizeof(int32_t), b->stream));
   return PH_OK;
 }
 
@@ -3434,7 +3555,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_slot_of_col, b->d_nonant_col, b->d_vals_s, b->d_dr, b->d_dc,
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
-                  b->d_ul, b->d_sb, b->d_part,
+                  b->d_ul, b->d_xpart, b->d_sb, b->d_part,
                   b->d_ctl, b->d_sym, b->d_ws, b->d_mlist, b->d_mctr,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
