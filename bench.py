@@ -191,9 +191,9 @@ def pdhg_flops_per_step(c):
 def hbm_config(args, world, farmer, PH, opts):
     """F3: farmer c=--hbm-crops, --scens scenarios per rank (the mid-size
     path: PDHG phase kernels mid_kernel and LDL' polish phases
-    mid_polish_kernel).  Iter0, one warmup
-    iteration, then --hbm-steps PH iterations through the device loop with
-    the library's per-launch HIP events.
+    mid_polish_kernel).  Iter0, --warmup PH
+    iterations (as the headline config), then --hbm-steps PH iterations
+    through the device loop with the library's per-launch HIP events.
 
     roofline: the solve (all its phase launches) as the unit -- algorithmic
     bytes = every scenario's data in and solution out (the bytes the solve
@@ -219,14 +219,16 @@ def hbm_config(args, world, farmer, PH, opts):
     torch.cuda.synchronize()
     t_iter0 = time.perf_counter() - t0
     nonopt0 = b.summary()[0]
-    ph.run_device_loop(0, 1, -1.0, chunk=1)
+    # the same warmup as the headline config (--warmup PH iterations)
+    wu = max(1, args.warmup)
+    ph.run_device_loop(0, wu, -1.0, chunk=1)
     ph.PHoptions["device_loop_graphs"] = False
     b.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ph.run_device_loop(1, 1 + args.hbm_steps, -1.0, chunk=args.hbm_steps)
+    ph.run_device_loop(wu, wu + args.hbm_steps, -1.0, chunk=args.hbm_steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     n_t, as_ms, po_ms, pd_ms, nk, k_ms, np_, p_ms = b.read_timing_full()

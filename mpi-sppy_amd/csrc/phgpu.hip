@@ -2674,6 +2674,13 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     const char *e = std::getenv("PHGPU_KKT_DELTA");
     b->md.delta = e ? std::atof(e) : KKT_DELTA;
   }
+  {  // PHGPU_KKT_REFINE_TOL: the polish's refinement stopping tolerance
+    const char *e = std::getenv("PHGPU_KKT_REFINE_TOL");
+    if (e) {
+      const double t = std::atof(e);
+      HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_refine_tol), &t, sizeof(t)));
+    }
+  }
   kd.pos = d + off[q++]; kd.Lcp = d + off[q++]; kd.Lri = d + off[q++]; kd.Lcl = d + off[q++];
   kd.Lrp = d + off[q++]; kd.Lrc = d + off[q++]; kd.Lrq = d + off[q++];
   kd.lvp = d + off[q++]; kd.lvc = d + off[q++]; kd.lep = d + off[q++]; kd.lee = d + off[q++];

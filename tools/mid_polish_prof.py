@@ -1,0 +1,42 @@
+"""GPU diagnostic: phase clocks of the mid-size LDL' polish (ph_debug_prof
+slots 9-15) over PH iterations of farmer S / c (eager device loop).
+
+    python tools/mid_polish_prof.py S C START NIT
+"""
+import ctypes
+import os
+import sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpi-sppy_amd"))
+import mpisppy_amd
+mpisppy_amd.disable_tictoc_output()
+from mpisppy_amd.opt.ph import PH
+from mpisppy_amd.examples import farmer
+
+S, C, START, NIT = (int(v) for v in sys.argv[1:5])
+opts = {"solvername": "mi355x_pdhg", "PHIterLimit": 100000, "defaultPHrho": 1.0,
+        "convthresh": -1, "verbose": False, "display_progress": False,
+        "iter0_solver_options": {}, "iterk_solver_options": {}, "device_loop_graphs": False}
+ph = PH(opts, [f"scen{i}" for i in range(S)], farmer.scenario_creator,
+        scenario_creator_kwargs={"crops_multiplier": C})
+ph.PH_Prep(); ph.subproblem_creation(); ph.Iter0()
+ph.run_device_loop(0, START, -1.0)
+b = ph.batch
+lib = b.lib
+lib.ph_debug_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+lib.ph_debug_prof.restype = ctypes.c_int32
+out = np.zeros(16, dtype=np.int64)
+lib.ph_debug_prof(b.handle, 1, None)
+b.set_timing(True)
+ph.run_device_loop(START, START + NIT, -1.0, chunk=NIT)
+t = b.read_timing_full()
+lib.ph_debug_prof(b.handle, 0, out.ctypes.data_as(ctypes.c_void_p))
+us = lambda v: v / 100.0  # 100 MHz ticks -> us (summed over blocks)
+npol = max(out[9], 1)
+print(f"iters {START}..{START+NIT}: mid_kernel {t[4]} launches {t[5]/max(t[4],1):.3f} ms avg, "
+      f"mid_polish {t[6]} launches {t[7]/max(t[6],1):.3f} ms avg")
+print(f"polishes {out[9]} ({out[9]/NIT:.0f}/iter), rounds {out[10]}, refinement solves {out[11]}, "
+      f"accepted {out[12]}")
+print(f"per polish (block-us): setup {us(out[15])/npol:.1f} factor {us(out[13])/npol:.1f} "
+      f"solves {us(out[14])/npol:.1f}")
