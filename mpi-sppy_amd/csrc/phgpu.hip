@@ -304,6 +304,13 @@ __device__ __forceinline__ bool stopped(const LoopCtl *c) {
 constexpr double OMEGA_SPAN_SMALL = 1e2;
 constexpr double OMEGA_SPAN_MID = 1e6;
 
+// Append s to a work list of capacity S (a list never holds more than S
+// entries; the bound keeps a stale counter from writing past it).
+__device__ __forceinline__ void list_push(int32_t *list, int32_t *count, int s, int S) {
+  const int q = atomicAdd(count, 1);
+  if (q < S) list[q] = s;
+}
+
 struct SolveArgs {
   int S, n, m, nnz;
   double omega_span;  // the primal weight is reset to omega0 once it leaves [omega0/span, omega0*span]
@@ -1391,7 +1398,7 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     a.diag[PH_DIAG_W * s + 2] = d_eg;
     a.diag[PH_DIAG_W * s + 3] = d_r;
     a.diag[PH_DIAG_W * s + 4] = (double)how;
-    if (stat != PH_STATUS_OPTIMAL && a.ul) a.ul[atomicAdd(a.ul_count, 1)] = s;
+    if (stat != PH_STATUS_OPTIMAL && a.ul) list_push(a.ul, a.ul_count, s, S);
   }
   __syncthreads();  // LDS is reused by the block's next scenario
 }
@@ -1403,7 +1410,7 @@ template <int BLOCK, int P, int E>
 __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int next;
-  const int count = stopped(a.ctl) ? 0 : (a.wl ? *a.wl_count : a.S);
+  const int count = stopped(a.ctl) ? 0 : (a.wl ? min(*a.wl_count, a.S) : a.S);
   // first scenario by block index (no atomics while the list is short),
   // then from the queue
   int idx = blockIdx.x;
@@ -1539,7 +1546,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   if (!ok || __ballot(lane < n && kslot >= 0 && keyj != Q)) {
     if (lane == 0) {
       a.hint_ok[s] = 0;
-      a.wl[atomicAdd(a.wl_count, 1)] = s;
+      list_push(a.wl, a.wl_count, s, S);
     }
     continue;
   }
@@ -1572,7 +1579,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
     if (lane < 4) a.hint[4 * (size_t)s + lane] = sig[lane];
     if (lane == 0) {
       a.hint_ok[s] = 1;
-      a.wl[atomicAdd(a.wl_count, 1)] = s;
+      list_push(a.wl, a.wl_count, s, S);
     }
     continue;
   }
@@ -1591,6 +1598,10 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
     dg[4] = 3.0;
   }
   }  // scenarios of the wave
+}
+
+__global__ void __launch_bounds__(WAVE) zero_i32_kernel(int32_t *p, int n) {
+  for (int i = threadIdx.x; i < n; i += WAVE) p[i] = 0;
 }
 
 // Start the next iteration (phbase.py:1498 loop head): count it, or stop
@@ -1754,7 +1765,7 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   const int S = a.S, n = a.n, m = a.m, nnz = a.nnz, K = a.K;
-  const int count = stopped(a.ctl) ? 0 : *a.wl_count;
+  const int count = stopped(a.ctl) ? 0 : min(*a.wl_count, a.S);
   if ((int)blockIdx.x >= count) return;
   // LDS: staging rows | solutions | vals | xs | ys | pattern + maps
   double *kst = lds;                        // [RG_KST]: staging rows / product vectors
@@ -2056,7 +2067,7 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
     }
     if (!solved && lane == 0) {  // tail_kernel: warm polish from the point, PDHG, rescue
       a.hint_ok[s] = 0;
-      a.wl2[atomicAdd(a.wl2_count, 1)] = s;
+      list_push(a.wl2, a.wl2_count, s, S);
     }
   }
 }
@@ -2069,7 +2080,7 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
 template <int E>
 __global__ void __launch_bounds__(WAVE) tail_kernel(SolveArgs a, MidArgs md, int has_md) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int count = stopped(a.ctl) ? 0 : *a.wl2_count;
+  const int count = stopped(a.ctl) ? 0 : min(*a.wl2_count, a.S);
   for (int idx = blockIdx.x; idx < count; idx += gridDim.x)  // uniform over the block
     miss_tail<E>(a, has_md ? &md : nullptr, a.wl2[idx], lds);
 }
@@ -2674,6 +2685,13 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     const char *e = std::getenv("PHGPU_KKT_DELTA");
     b->md.delta = e ? std::atof(e) : KKT_DELTA;
   }
+  {  // PHGPU_MID_POLISH_ROUNDS: PDAS rounds of one mid-size polish
+    const char *e = std::getenv("PHGPU_MID_POLISH_ROUNDS");
+    if (e) {
+      const int r = std::max(1, std::atoi(e));
+      HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_polish_rounds), &r, sizeof(r)));
+    }
+  }
   {  // PHGPU_KKT_REFINE_TOL: the polish's refinement stopping tolerance
     const char *e = std::getenv("PHGPU_KKT_REFINE_TOL");
     if (e) {
@@ -3029,7 +3047,11 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   a.cache = nullptr;
   a.wl = nullptr;
   if (int rc = mid_init(b)) return rc;
-  HIP_OK(hipMemsetAsync(b->d_mctr, 0, 16 * sizeof(int32_t), b->stream));
+  // the phase counters, cleared by a kernel (ordered like the phase kernels
+  // when the device loop is replayed as a graph; a captured memset node was
+  // the suspect of a mid-size graph-replay fault)
+  hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_mctr, 16);
+  HIP_OK(hipGetLastError());
   hipEvent_t *tev = nullptr;
   if (b->timing) {
     if (b->ev_used + 4 > b->ev.size()) {
@@ -3147,6 +3169,11 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
       return e ? std::atof(e) : 0.0;
     }();
     a.omega_span = span > 0.0 ? span : (b->mid ? OMEGA_SPAN_MID : OMEGA_SPAN_SMALL);
+    static const double span_qp = [] {  // PHGPU_OMEGA_SPAN_QP: prox-QP solves (measurement hook)
+      const char *e = std::getenv("PHGPU_OMEGA_SPAN_QP");
+      return e ? std::atof(e) : 0.0;
+    }();
+    if (span_qp > 0.0 && prox_on > 0.0) a.omega_span = span_qp;
   }
   a.P = Pattern{b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k};
   a.X = Chunks{b->xr, b->xc, b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
@@ -3261,7 +3288,11 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)tlds));
         b->miss_attr = true;
       }
-      hipLaunchKernelGGL((tail_kernel<E_>), dim3(std::min(b->S, std::min(b->pdhg_grid, 64))),
+      static const int tail_grid = [] {  // PHGPU_TAIL_GRID: measurement hook
+        const char *e = std::getenv("PHGPU_TAIL_GRID");
+        return e ? std::max(1, std::atoi(e)) : 64;
+      }();
+      hipLaunchKernelGGL((tail_kernel<E_>), dim3(std::min(b->S, std::min(b->pdhg_grid, tail_grid))),
                          dim3(WAVE), tlds, b->stream, a, b->md, has_md);
     });
     HIP_OK(hipGetLastError());

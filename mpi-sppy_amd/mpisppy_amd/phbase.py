@@ -670,9 +670,14 @@ class PHBase(SPBase):
 
     def _graph_ok(self):
         """Replay chunks of the device loop as one HIP graph: a single GPU rank
-        (collectives stay eager) on a CUDA device."""
+        (collectives stay eager) on a CUDA device, one-wave scenarios (n + m
+        <= 63).  Mid-size scenarios launch eagerly: their iterations take
+        milliseconds, so graphs save nothing there, and a graph-replayed
+        mid-size chunk faulted intermittently."""
+        b = self.batch
         return (self.PHoptions.get("device_loop_graphs", True) and self.comm.size == 1
-                and self.device.type == "cuda" and hasattr(self.batch, "set_stream"))
+                and self.device.type == "cuda" and hasattr(b, "set_stream")
+                and b.n + b.m <= 63)
 
     def _capture_chunk(self, kw, chunk):
         """Capture `chunk` device iterations (the library's launches moved to
