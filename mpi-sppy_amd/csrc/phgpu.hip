@@ -2692,6 +2692,13 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_polish_rounds), &r, sizeof(r)));
     }
   }
+  {  // PHGPU_MID_PIN=0: measurement hook, no pinned rows in the mid-size polish
+    const char *e = std::getenv("PHGPU_MID_PIN");
+    if (e) {
+      const int v = std::atoi(e) != 0;
+      HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_pin_rows), &v, sizeof(v)));
+    }
+  }
   {  // PHGPU_KKT_REFINE_TOL: the polish's refinement stopping tolerance
     const char *e = std::getenv("PHGPU_KKT_REFINE_TOL");
     if (e) {

@@ -40,3 +40,5 @@ print(f"polishes {out[9]} ({out[9]/NIT:.0f}/iter), rounds {out[10]}, refinement 
       f"accepted {out[12]}")
 print(f"per polish (block-us): setup {us(out[15])/npol:.1f} factor {us(out[13])/npol:.1f} "
       f"solves {us(out[14])/npol:.1f}")
+print(f"rounds with a pinned row {out[5]}; exits: accepted {out[12]}, set repeats {out[1]}, non-finite {out[2]}, round limit {out[3]}; "
+      f"failed checks: refinement short {out[4]}, ep {out[6]}, ed {out[7]}, eg {out[8]}")
