@@ -3009,6 +3009,16 @@ static int phase_event(ph_batch *b, int kind) {
   return PH_OK;
 }
 
+// PHGPU_MID_FULLGRID=1: measurement hook, the phase kernels launched over S
+// blocks (one scenario each) instead of the resident grid
+static bool mid_full_grid() {
+  static const bool f = [] {
+    const char *e = std::getenv("PHGPU_MID_FULLGRID");
+    return e && std::atoi(e) != 0;
+  }();
+  return f;
+}
+
 // First-use setup of the mid-size kernels: LDS limits, occupancy, the HBM
 // polish workspace (when it does not fit in LDS), the work lists.
 static int mid_init(ph_batch *b) {
@@ -3079,7 +3089,8 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     const MidPhase ph{in, cin, out, cout, q, exit_err, first, 0, hand_at_limit};
     if (int rc = phase_event(b, 0)) return rc;
     DISPATCH_MID({
-      hipLaunchKernelGGL((mid_kernel<B_, C_, R_>), dim3(b->S), dim3(B_), b->mid_lds_bytes,
+      hipLaunchKernelGGL((mid_kernel<B_, C_, R_>), dim3(mid_full_grid() ? b->S : b->mid_grid), dim3(B_),
+                         b->mid_lds_bytes,
                          b->stream, a, b->md, ph, b->mid_lds_doubles);
     });
     HIP_OK(hipGetLastError());
@@ -3090,7 +3101,8 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode, 0, 0};
     if (int rc = phase_event(b, 1)) return rc;
     DISPATCH_MID({
-      hipLaunchKernelGGL((mid_polish_kernel<B_, C_, R_>), dim3(b->S), dim3(B_),
+      hipLaunchKernelGGL((mid_polish_kernel<B_, C_, R_>), dim3(mid_full_grid() ? b->S : b->mid_pgrid),
+                         dim3(B_),
                          b->mid_plds_bytes, b->stream, a, b->md, ph, b->mid_lds_doubles);
     });
     HIP_OK(hipGetLastError());
