@@ -280,6 +280,52 @@ def hbm_config(args, world, farmer, PH, opts):
                                              "from HBM would need -- a work rate, not a measurement"}}
 
 
+def sslp_config(args, world, PH, opts):
+    """BASELINE config 5: sslp_15_45 LP relaxation (n=705, m=60, nnz=1364 per
+    scenario; synthetic scenarios, ClientPresent ~ Bernoulli(0.5) seeded per
+    scenario, `mpisppy_amd/examples/sslp.py`), --sslp-scens per rank, rho 1.  Iter0, --warmup PH
+    iterations, then --hbm-steps timed PH iterations through the device loop
+    (eager: mid-size batch)."""
+    from mpisppy_amd.examples import sslp as ex
+    S = args.sslp_scens * world
+    o = dict(opts)
+    ph = PH(o, ex.scenario_names(S), ex.scenario_creator,
+            scenario_creator_kwargs={"instance": "sslp_15_45_synthetic"})
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    ph._create_solvers()
+    b = ph.batch
+    torch.cuda.synchronize()
+    _progress("sslp Iter0")
+    t0 = time.perf_counter()
+    ph.Iter0()
+    torch.cuda.synchronize()
+    t_iter0 = time.perf_counter() - t0
+    nonopt0 = b.summary()[0]
+    wu = max(1, args.warmup)
+    ph.run_device_loop(0, wu, -1.0, chunk=1)
+    ph.PHoptions["device_loop_graphs"] = False
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ph.run_device_loop(wu, wu + args.hbm_steps, -1.0, chunk=args.hbm_steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = b.loop_status()
+    d = torch.tensor([dt], dtype=torch.float64, device=_red_dev())
+    if world > 1:
+        dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    dt = float(d.item())
+    return {"workload": f"sslp_15_45 LP relaxation PH, {S} synthetic scenarios ({args.sslp_scens} "
+                        f"per GPU), n={b.n}, m={b.m}, nnz={b.nnz} per scenario, rho=1",
+            "value": round(S * args.hbm_steps / dt, 2), "unit": "solves/s",
+            "ms_per_step": round(dt / args.hbm_steps * 1000.0, 3), "steps": args.hbm_steps,
+            "warmup": wu, "iter0_s": round(t_iter0, 3), "iter0_not_optimal": nonopt0,
+            "not_optimal_in_window": st[2],
+            "pdhg_steps_per_solve": round(st[4] / max(st[3], 1), 1), "pdhg_steps_max": st[5]}
+
+
 def _spawn_ranks(n, cpu):
     """`bench.py --gpus N` without a launcher: this parent (which has not
     touched the GPU) starts N rank processes, one per GPU, with the
@@ -366,6 +412,8 @@ def _parser():
     ap.add_argument("--hbm-crops", type=int, default=100,
                     help="crops_multiplier of the HBM-bound companion config (F3); 0 = skip")
     ap.add_argument("--hbm-steps", type=int, default=5)
+    ap.add_argument("--sslp-scens", type=int, default=10000,
+                    help="scenarios per rank of the sslp companion config (BASELINE config 5); 0 = skip")
     return ap
 
 
@@ -550,6 +598,11 @@ def run():
         f3 = hbm_config(args, world, farmer, PH, opts)
 
 
+    sslp = None
+    if args.sslp_scens > 0:
+        _progress("companion config sslp")
+        sslp = sslp_config(args, world, PH, opts)
+
     if rank == 0:
         value = S * args.steps / dt
         n, m, nnz = farmer_dims(c)
@@ -597,6 +650,7 @@ def run():
             "ph_to_tol_sample": tol_small,
             "cpu_baseline": cpu,
             "hbm_config": f3,
+            "sslp_config": sslp,
         }
     else:
         out = None
