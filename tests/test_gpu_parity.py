@@ -472,19 +472,21 @@ def test_hydro_ph_trajectory_from_oracle_iter0_point():
     assert abs(eobj - oe) <= 1e-5 * abs(oe)
 
 
-def test_farmer_c100_mid_path_matches_oracle():
+@pytest.mark.parametrize("iters", [6, 12])
+def test_farmer_c100_mid_path_matches_oracle(iters):
     """BASELINE's HBM-regime scenario shape (farmer crops_multiplier 100:
     1200 columns, 901 rows, 2700 nonzeros, one 300-entry row) through the
     mid-size path (mid_kernel / mid_polish_kernel, 1024-thread blocks, the
     quasi-definite LDL' active-set polish) against the oracle: 12 scenarios
     from scen3 (scen0-2 have identical yields across the crop copies, a
-    non-unique Iter0 optimum), 6 PH iterations.  Trivial bound 1e-7,
-    Eobj / x-bar / W 1e-5 elementwise, equal iteration count
-    (phbase.py:1364-1566)."""
+    non-unique Iter0 optimum), 6 and 12 PH iterations (12: past the point
+    where, at 10k scenarios, the warm polish met degenerate vertices and
+    pins rows).  Trivial bound 1e-7, Eobj / x-bar / W 1e-5
+    elementwise, equal iteration count (phbase.py:1364-1566)."""
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     names = [f"scen{i}" for i in range(3, 15)]
-    opts = _opts(PHIterLimit=6, defaultPHrho=1.0, convthresh=1e-7)
+    opts = _opts(PHIterLimit=iters, defaultPHrho=1.0, convthresh=1e-7)
     ph = PH(dict(opts), names, farmer.scenario_creator,
             scenario_creator_kwargs={"crops_multiplier": 100})
     conv, eobj, tb = ph.ph_main()
