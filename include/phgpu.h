@@ -12,7 +12,11 @@
  *
  * Error model: every int-returning call returns 0 on success, or
  *   PH_EINVAL (-1) invalid argument, PH_EHIP (-2) HIP runtime error,
- *   PH_ENUM (-3) numerical failure.
+ *   PH_ENUM (-3) numerical failure, PH_EDEV (-4) a device-side invariant
+ *   check failed in an earlier launch (a work list or workspace index out of
+ *   range; the offending access was skipped, the batch's results are not to
+ *   be trusted; reported by the synchronising calls ph_batch_solve_summary,
+ *   ph_loop_status and ph_batch_sync).
  * ph_last_error() returns a thread-local message for the last failure.
  * Calls are stream-ordered on the stream given to ph_batch_create /
  * ph_batch_set_stream and return without synchronising unless stated.
@@ -30,6 +34,7 @@ extern "C" {
 #define PH_EINVAL (-1)
 #define PH_EHIP (-2)
 #define PH_ENUM (-3)
+#define PH_EDEV (-4)
 
 /* per-scenario solve status (phbase.py:959-989 maps 2/3 -> infeasible) */
 #define PH_STATUS_OPTIMAL 0

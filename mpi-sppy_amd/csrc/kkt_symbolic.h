@@ -20,6 +20,7 @@
 #pragma once
 
 #include <algorithm>
+#include <climits>
 #include <cstdint>
 #include <queue>
 #include <utility>
@@ -29,6 +30,9 @@ struct KktSymbolic {
   int n = 0, m = 0, N = 0, nnzL = 0, NL = 0;
   int chain0 = 0;  // levels chain0 .. NL-1 hold one column each (the top of the tree)
   long ncontrib = 0;
+  const char *error = nullptr;  // why analyze() refused the pattern
+  // the update lists' size a pattern may need at most (three int32 arrays)
+  static constexpr long long kMaxContrib = 1LL << 28;
   std::vector<int32_t> pos;              // [N] vertex -> permuted index
   std::vector<int32_t> Lcp, Lri, Lcl;    // CSC of the strict lower triangle of L; column of entry
   std::vector<int32_t> Lrp, Lrc, Lrq;    // CSR view: row r -> columns k, CSC positions
@@ -92,7 +96,10 @@ struct KktSymbolic {
       }
       g[v].clear();
     }
-    if ((int)order.size() != N) return false;
+    if ((int)order.size() != N) {
+      error = "the minimum-degree order did not cover every vertex";
+      return false;
+    }
     pos.assign(N, 0);
     for (int c = 0; c < N; ++c) pos[order[c]] = c;
     // ---- symbolic factorisation: pattern(c) = {pos[a] > c} U children's patterns
@@ -118,6 +125,23 @@ struct KktSymbolic {
       if (!P.empty()) {
         parent[c] = P[0];
         kids[P[0]].push_back(c);
+      }
+    }
+    {  // sizes in 64 bits first: a dense trailing block of a few thousand
+       // vertices overflows int32 in the update lists
+      long long nl = 0, nc = 0;
+      for (int c = 0; c < N; ++c) {
+        const long long sz = (long long)pat[c].size();
+        nl += sz;
+        nc += sz * (sz - 1) / 2;
+      }
+      if (nl > INT32_MAX) {
+        error = "the KKT factor has more than 2^31 entries";
+        return false;
+      }
+      if (nc > kMaxContrib) {
+        error = "the KKT factor's update lists exceed 2^28 entries";
+        return false;
       }
     }
     Lcp.assign(N + 1, 0);

@@ -304,11 +304,51 @@ __device__ __forceinline__ bool stopped(const LoopCtl *c) {
 constexpr double OMEGA_SPAN_SMALL = 1e2;
 constexpr double OMEGA_SPAN_MID = 1e6;
 
+// Device-side invariant checks.  A violated invariant (a work list pushed
+// past its capacity, a count above S, a list entry or workspace slice out of
+// range) is recorded in the batch's error words err[4] = {code, v0, v1, -}
+// (the first one wins) and the offending access is skipped; the host turns
+// a recorded violation into PH_EDEV at its next synchronising call
+// (ph_batch_solve_summary, ph_loop_status, ph_batch_sync).
+enum DevCheck : int32_t {
+  CHK_LIST_OVERFLOW = 1,  // push into a full work list (v0 = ticket, v1 = S)
+  CHK_COUNT_RANGE = 2,    // a list count above S (v0 = count, v1 = S)
+  CHK_ENTRY_RANGE = 3,    // a list entry outside [0, S) (v0 = entry, v1 = list index)
+  CHK_WS_RANGE = 4,       // a block past the HBM polish workspace (v0 = block, v1 = slices)
+  CHK_QUEUE_RANGE = 5,    // a queue ticket below the grid (v0 = index, v1 = grid)
+};
+__device__ __forceinline__ void dev_fail(int32_t *err, int code, int v0, int v1) {
+  if (err && atomicCAS(err, 0, code) == 0) {
+    err[1] = v0;
+    err[2] = v1;
+  }
+}
+
 // Append s to a work list of capacity S (a list never holds more than S
-// entries; the bound keeps a stale counter from writing past it).
-__device__ __forceinline__ void list_push(int32_t *list, int32_t *count, int s, int S) {
+// entries: a ticket past it is an invariant violation, recorded, and the
+// store skipped).
+__device__ __forceinline__ void list_push(int32_t *list, int32_t *count, int s, int S, int32_t *err) {
   const int q = atomicAdd(count, 1);
   if (q < S) list[q] = s;
+  else dev_fail(err, CHK_LIST_OVERFLOW, q, S);
+}
+
+// The entries of a work list to take: min(*count, S) (a count above S is
+// recorded as a violation by thread 0 of block 0).
+__device__ __forceinline__ int list_count(const int32_t *count, int S, int32_t *err) {
+  const int c = *count;
+  if (c > S && threadIdx.x == 0 && blockIdx.x == 0) dev_fail(err, CHK_COUNT_RANGE, c, S);
+  return min(c, S);
+}
+
+// Entry idx of a work list, checked against [0, S): -1 (skip) when outside.
+__device__ __forceinline__ int list_entry(const int32_t *list, int idx, int S, int32_t *err) {
+  const int s = list[idx];
+  if (s < 0 || s >= S) {
+    if (threadIdx.x == 0) dev_fail(err, CHK_ENTRY_RANGE, s, idx);
+    return -1;
+  }
+  return s;
 }
 
 struct SolveArgs {
@@ -350,6 +390,7 @@ struct SolveArgs {
   int32_t *ul, *ul_count;
   const LoopCtl *ctl;  // device loop control or null
   unsigned long long *prof;  // [16] phase clocks of the warm polish, or null
+  int32_t *err;              // [4] device-side invariant checks (dev_fail)
 };
 
 // Active-set polish: largest KKT system (free columns + active rows) and the
@@ -1398,7 +1439,7 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     a.diag[PH_DIAG_W * s + 2] = d_eg;
     a.diag[PH_DIAG_W * s + 3] = d_r;
     a.diag[PH_DIAG_W * s + 4] = (double)how;
-    if (stat != PH_STATUS_OPTIMAL && a.ul) list_push(a.ul, a.ul_count, s, S);
+    if (stat != PH_STATUS_OPTIMAL && a.ul) list_push(a.ul, a.ul_count, s, S, a.err);
   }
   __syncthreads();  // LDS is reused by the block's next scenario
 }
@@ -1410,12 +1451,13 @@ template <int BLOCK, int P, int E>
 __global__ void __launch_bounds__(BLOCK) pdhg_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int next;
-  const int count = stopped(a.ctl) ? 0 : (a.wl ? min(*a.wl_count, a.S) : a.S);
+  const int count = stopped(a.ctl) ? 0 : (a.wl ? list_count(a.wl_count, a.S, a.err) : a.S);
   // first scenario by block index (no atomics while the list is short),
   // then from the queue
   int idx = blockIdx.x;
   while (idx < count) {  // uniform over the block
-    solve_scenario<BLOCK, P, E>(a, a.wl ? a.wl[idx] : idx, lds);
+    const int s = a.wl ? list_entry(a.wl, idx, a.S, a.err) : idx;
+    if (s >= 0) solve_scenario<BLOCK, P, E>(a, s, lds);
     if (threadIdx.x == 0) next = (int)gridDim.x + atomicAdd(a.queue, 1);
     __syncthreads();
     idx = next;
@@ -1546,7 +1588,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   if (!ok || __ballot(lane < n && kslot >= 0 && keyj != Q)) {
     if (lane == 0) {
       a.hint_ok[s] = 0;
-      list_push(a.wl, a.wl_count, s, S);
+      list_push(a.wl, a.wl_count, s, S, a.err);
     }
     continue;
   }
@@ -1579,7 +1621,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
     if (lane < 4) a.hint[4 * (size_t)s + lane] = sig[lane];
     if (lane == 0) {
       a.hint_ok[s] = 1;
-      list_push(a.wl, a.wl_count, s, S);
+      list_push(a.wl, a.wl_count, s, S, a.err);
     }
     continue;
   }
@@ -1765,7 +1807,7 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   const int S = a.S, n = a.n, m = a.m, nnz = a.nnz, K = a.K;
-  const int count = stopped(a.ctl) ? 0 : min(*a.wl_count, a.S);
+  const int count = stopped(a.ctl) ? 0 : list_count(a.wl_count, a.S, a.err);
   if ((int)blockIdx.x >= count) return;
   // LDS: staging rows | solutions | vals | xs | ys | pattern + maps
   double *kst = lds;                        // [RG_KST]: staging rows / product vectors
@@ -1809,7 +1851,8 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
     }
   };
   for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
-    const int s = a.wl[idx];
+    const int s = list_entry(a.wl, idx, S, a.err);
+    if (s < 0) continue;  // (uniform: one wave)
     __syncthreads();  // LDS of the previous scenario
     tick(9);  // pattern copy / previous scenario's tail
     // ---- scenario data (scaled): static block, PH terms, values
@@ -2067,7 +2110,7 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
     }
     if (!solved && lane == 0) {  // tail_kernel: warm polish from the point, PDHG, rescue
       a.hint_ok[s] = 0;
-      list_push(a.wl2, a.wl2_count, s, S);
+      list_push(a.wl2, a.wl2_count, s, S, a.err);
     }
   }
 }
@@ -2080,9 +2123,12 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
 template <int E>
 __global__ void __launch_bounds__(WAVE) tail_kernel(SolveArgs a, MidArgs md, int has_md) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int count = stopped(a.ctl) ? 0 : min(*a.wl2_count, a.S);
-  for (int idx = blockIdx.x; idx < count; idx += gridDim.x)  // uniform over the block
-    miss_tail<E>(a, has_md ? &md : nullptr, a.wl2[idx], lds);
+  const int count = stopped(a.ctl) ? 0 : list_count(a.wl2_count, a.S, a.err);
+  if (count <= (int)blockIdx.x || (has_md && !ws_block_ok(md, a.err))) return;
+  for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {  // uniform over the block
+    const int s = list_entry(a.wl2, idx, a.S, a.err);
+    if (s >= 0) miss_tail<E>(a, has_md ? &md : nullptr, s, lds);
+  }
 }
 
 
@@ -2245,13 +2291,37 @@ constexpr int POST_COMB = 2048;  // LDS doubles of a combine chunk
 // chunks, combined by the last block (XbarArgs).
 // A reduction instead of per-workgroup atomics on one address, which
 // serialise 10k+ workgroups at the end of the solve.
+// The chunked form's end: every block (block 0 and the G*C chunk blocks)
+// takes a ticket after its work; the block that takes the last one sums
+// the chunk partials in chunk order (deterministic) and advances the
+// iteration.  Every block has passed its stop check by then, so an advance
+// that stops the loop (the limit) cannot make a block skip its work
+// (block 0's counts included) half way through the launch.
+__device__ __forceinline__ void summary_last(const XbarArgs &xa, LoopCtl *ctl) {
+  if (!last_block(xa.ticket)) return;
+  for (int gg = threadIdx.x; gg < xa.G; gg += blockDim.x) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int cc = 0; cc < xa.C; ++cc) {  // chunk order: deterministic
+      a0 += sub(xa.part + 2 * ((size_t)gg * xa.C + cc));
+      a1 += sub(xa.part + 2 * ((size_t)gg * xa.C + cc) + 1);
+    }
+    xa.out[gg] = a0;
+    xa.out[xa.G + gg] = a1;
+  }
+  if (threadIdx.x == 0) {
+    reset_ticket(xa.ticket);
+    if (ctl) loop_advance(ctl);
+  }
+}
+
 __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__restrict__ status,
                                                        const int32_t *__restrict__ iters,
                                                        const double *__restrict__ diag,
                                                        unsigned long long *__restrict__ out,
                                                        LoopCtl *ctl, XbarArgs xa,
                                                        const int32_t *__restrict__ ctr,
-                                                       const int32_t *__restrict__ wl2) {
+                                                       const int32_t *__restrict__ wl2,
+                                                       int32_t *err) {
   __shared__ unsigned long long red[5][MAX_WAVES];
   if (stopped(ctl)) return;
   if (blockIdx.x > 0 && xa.C == 0) {  // device loop, one block per node slot
@@ -2268,47 +2338,27 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
       pub(xa.part + 2 * (size_t)b, v[0]);
       pub(xa.part + 2 * (size_t)b + 1, v[1]);
     }
-    // (the ticket counts the G*C chunk blocks only)
-    __shared__ int last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      last = __hip_atomic_fetch_add(xa.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             xa.G * xa.C - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    for (int gg = threadIdx.x; gg < xa.G; gg += blockDim.x) {
-      double a0 = 0.0, a1 = 0.0;
-      for (int cc = 0; cc < xa.C; ++cc) {  // chunk order: deterministic
-        a0 += sub(xa.part + 2 * ((size_t)gg * xa.C + cc));
-        a1 += sub(xa.part + 2 * ((size_t)gg * xa.C + cc) + 1);
-      }
-      xa.out[gg] = a0;
-      xa.out[xa.G + gg] = a1;
-    }
-    if (threadIdx.x == 0) {
-      reset_ticket(xa.ticket);
-      // the iteration advances here, after every chunk block has passed its
-      // stop check (block 0 advancing could stop blocks that have not
-      // started, and their tickets would be missing)
-      if (ctl) loop_advance(ctl);
-    }
+    summary_last(xa, ctl);
     return;
   }
   unsigned long long v[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
   const int bd = blockDim.x;
-  const int nl = ctr ? ctr[2] : S;  // scenarios to scan
+  // scenarios to scan (the counts clamped to S: a count past it is a
+  // violation list_count records)
+  const int nl = ctr ? list_count(ctr + 2, S, err) : S;
   for (int s0 = threadIdx.x; s0 < nl; s0 += 4 * bd) {
     int st[4], itr[4];
     double hw[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {  // independent loads in flight
       const int q = s0 + u * bd;
-      const int s = q < nl ? (ctr ? wl2[q] : q) : 0;
-      st[u] = q < nl ? status[s] : PH_STATUS_OPTIMAL;
-      itr[u] = q < nl ? iters[s] : 0;
-      hw[u] = q < nl ? diag[PH_DIAG_W * (size_t)s + 4] : 0.0;
+      int s = q < nl ? (ctr ? wl2[q] : q) : 0;
+      const bool in = q < nl && s >= 0 && s < S;
+      if (q < nl && !in) dev_fail(err, CHK_ENTRY_RANGE, s, q);
+      if (!in) s = 0;
+      st[u] = in ? status[s] : PH_STATUS_OPTIMAL;
+      itr[u] = in ? iters[s] : 0;
+      hw[u] = in ? diag[PH_DIAG_W * (size_t)s + 4] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -2340,8 +2390,9 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
       out[i] = t;
     }
     if (ctr) {  // the scenarios the cache and the register polish finished
-      out[3] += (unsigned long long)(ctr[0] - ctr[2]);
-      out[4] += (unsigned long long)(S - ctr[0]);
+      const int c0 = list_count(ctr, S, err);
+      out[3] += (unsigned long long)max(c0 - nl, 0);
+      out[4] += (unsigned long long)(S - c0);
     }
     if (ctl) {  // running totals of the device loop, then the next iteration
       ctl->acc[0] += out[0];
@@ -2350,9 +2401,10 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
       ctl->acc[3] = out[2] > ctl->acc[3] ? out[2] : ctl->acc[3];
       ctl->acc[4] += out[3];
       ctl->acc[5] += out[4];
-      if (gridDim.x == 1 || xa.C == 0) loop_advance(ctl);  // else the last chunk block advances
+      if (gridDim.x == 1 || xa.C == 0) loop_advance(ctl);  // else the last block advances
     }
   }
+  if (gridDim.x > 1 && xa.C > 0) summary_last(xa, ctl);
 }
 
 // Single-rank device loop: Compute_Xbar's broadcast + Update_W (as
@@ -2497,6 +2549,7 @@ struct ph_batch {
   int mid_grid = 0, mid_pgrid = 0;  // resident blocks of the PDHG / polish phase kernels
   int32_t *d_mlist = nullptr;  // [5][S] phase work lists
   int32_t *d_mctr = nullptr;   // [16] list counts (0..4) and queue counters (8..13)
+  int32_t *d_err = nullptr;    // [4] device-side invariant checks (dev_fail)
 };
 
 namespace {
@@ -2532,10 +2585,10 @@ bool pick_geometry(int n, int m, int xr, int xc, int *block, int *per, int *ext)
 
 #define DISPATCH_EXT(BLK, PER, EXT, ...)                                              \
   do {                                                                               \
-    if (EXT == 0) { constexpr int B_ = BLK, P_ = PER, E_ = 0; (void)E_; __VA_ARGS__; }          \
-    else if (EXT == 1) { constexpr int B_ = BLK, P_ = PER, E_ = 1; (void)E_; __VA_ARGS__; }     \
-    else if (EXT == 2) { constexpr int B_ = BLK, P_ = PER, E_ = 2; (void)E_; __VA_ARGS__; }     \
-    else { constexpr int B_ = BLK, P_ = PER, E_ = 4; (void)E_; __VA_ARGS__; }                   \
+    if (EXT == 0) { constexpr int B_ = BLK, P_ = PER, E_ = 0; (void)B_; (void)P_; (void)E_; __VA_ARGS__; }      \
+    else if (EXT == 1) { constexpr int B_ = BLK, P_ = PER, E_ = 1; (void)B_; (void)P_; (void)E_; __VA_ARGS__; } \
+    else if (EXT == 2) { constexpr int B_ = BLK, P_ = PER, E_ = 2; (void)B_; (void)P_; (void)E_; __VA_ARGS__; } \
+    else { constexpr int B_ = BLK, P_ = PER, E_ = 4; (void)B_; (void)P_; (void)E_; __VA_ARGS__; }               \
   } while (0)
 
 #define DISPATCH_GEOM(BLK, PER, EXT, ...)                                              \
@@ -2647,6 +2700,25 @@ void build_tails(int lines, const int32_t *ptr, int BLOCK, std::vector<int32_t> 
 
 static LoopCtl *loop_ctl(const ph_batch *b) { return b->loop_on ? b->d_ctl : nullptr; }
 
+// The synchronising calls copy the device-side check words with their
+// own result (one stream synchronisation for both); a violation (dev_fail)
+// recorded by any earlier launch becomes PH_EDEV (sticky: the batch's
+// results are not to be trusted after one).
+static int queue_err_copy(ph_batch *b, int32_t (&e)[4]) {
+  HIP_OK(hipMemcpyAsync(e, b->d_err, sizeof(e), hipMemcpyDeviceToHost, b->stream));
+  return PH_OK;
+}
+static int check_dev(const int32_t (&e)[4]) {
+  if (e[0] == 0) return PH_OK;
+  static const char *what[] = {"?", "work list pushed past its capacity S",
+                               "work-list count above S", "work-list entry outside [0, S)",
+                               "block past the HBM polish workspace", "work-queue ticket out of range"};
+  char msg[256];
+  std::snprintf(msg, sizeof(msg), "device-side check failed: %s (code %d, values %d %d)",
+                what[(e[0] >= 1 && e[0] <= 5) ? e[0] : 0], e[0], e[1], e[2]);
+  return fail(PH_EDEV, msg);
+}
+
 // Symbolic analysis of the KKT pattern, the tails of long lines and the
 // LDS plan of the mid-size path; uploads the index arrays (one buffer).
 static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx,
@@ -2655,7 +2727,8 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns; the "
                            "on-chip solver does not cover it");
   if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx))
-    return fail(PH_ENUM, "ph_batch_create: KKT symbolic analysis failed");
+    return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
+                               (b->sym.error ? b->sym.error : "?"));
   const KktSymbolic &y = b->sym;
   std::vector<int32_t> rwp, rtb, rln, rbb, rtp, cwp, ctb, cln, cbb, ctp;
   build_tails(b->m, row_ptr, b->mblock, rwp, rtb, rln, rbb, rtp);
@@ -2809,6 +2882,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
       (rc = dalloc(&b->d_u, (size_t)S * n)) || (rc = dalloc(&b->d_rl, (size_t)S * m)) ||
       (rc = dalloc(&b->d_ru, (size_t)S * m)) || (rc = dalloc(&b->d_diag, (size_t)S * PH_DIAG_W)) ||
       (rc = dalloc(&b->d_summary, 5)) || (rc = dalloc(&b->d_ctr, 8)) || (rc = dalloc(&b->d_ctl, 1)) ||
+      (rc = dalloc(&b->d_err, 4)) ||
       (rc = dalloc(&b->d_ul, S)) || (rc = dalloc(&b->d_r_pb, m + 1)) || (rc = dalloc(&b->d_r_pos, b->xr)) ||
       (rc = dalloc(&b->d_r_len, b->xr)) || (rc = dalloc(&b->d_c_pb, n + 1)) ||
       (rc = dalloc(&b->d_c_pos, b->xc)) || (rc = dalloc(&b->d_c_len, b->xc))) {
@@ -2820,7 +2894,8 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
     ph_batch_destroy(b);
     return fail(PH_EHIP, "ph_batch_create: allocation failed");
   }
-  if (hipMemsetAsync(b->d_ctr, 0, 8 * sizeof(int32_t), b->stream) != hipSuccess) {
+  if (hipMemsetAsync(b->d_ctr, 0, 8 * sizeof(int32_t), b->stream) != hipSuccess ||
+      hipMemsetAsync(b->d_err, 0, 4 * sizeof(int32_t), b->stream) != hipSuccess) {
     ph_batch_destroy(b);
     return fail(PH_EHIP, "ph_batch_create: clearing counters failed");
   }
@@ -3040,9 +3115,23 @@ static int mid_init(ph_batch *b) {
     return fail(PH_EINVAL, "ph_pdhg_solve: the mid-size kernels cannot be resident");
   b->mid_grid = std::min(b->S, per_cu * std::max(1, cus));
   b->mid_pgrid = std::min(b->S, per_cu_p * std::max(1, cus));
-  const int wg = b->S;  // one block per scenario: the workspace slice of block b
+  {  // PHGPU_MID_GRID: cap the resident grid (read per batch; the parity
+     // tests push several scenarios through each block's work-queue loop
+     // and its workspace slice with a small grid)
+    const char *e = std::getenv("PHGPU_MID_GRID");
+    const int cap = e ? std::atoi(e) : 0;
+    if (cap > 0) {
+      b->mid_grid = std::min(b->mid_grid, cap);
+      b->mid_pgrid = std::min(b->mid_pgrid, cap);
+    }
+  }
+  // the HBM polish workspace: one slice per block of every launch that runs
+  // the polish (mid_polish_kernel; on one-wave batches rescue_kernel and
+  // tail_kernel), not one per scenario
+  b->md.ws_blocks = mid_full_grid() ? b->S
+                                    : std::max({b->mid_grid, b->mid_pgrid, std::min(b->S, TAIL_GRID)});
   if (b->md.ws_stride > 0) {
-    int rc = dalloc(&b->d_ws, (size_t)wg * b->md.ws_stride);
+    int rc = dalloc(&b->d_ws, (size_t)b->md.ws_blocks * b->md.ws_stride);
     if (rc) return rc;
     b->md.ws_g = b->d_ws;
   }
@@ -3138,7 +3227,7 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   const int post_g = (b->loop_on && b->loop_xa.x == a.x) ? b->loop_xa.G * std::max(1, b->loop_xa.C) : 0;
   hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, a.status,
                      a.iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa,
-                     (const int32_t *)nullptr, (const int32_t *)nullptr);
+                     (const int32_t *)nullptr, (const int32_t *)nullptr, b->d_err);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -3225,6 +3314,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.ul_count = b->d_ctr + 6;
   a.ctl = loop_ctl(b);
   a.prof = b->d_prof;
+  a.err = b->d_err;
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   if (b->mid) return mid_solve(b, a, opts);
   const size_t lds = solve_lds_bytes(b);
@@ -3309,7 +3399,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
       }
       static const int tail_grid = [] {  // PHGPU_TAIL_GRID: measurement hook
         const char *e = std::getenv("PHGPU_TAIL_GRID");
-        return e ? std::max(1, std::atoi(e)) : 64;
+        return e ? std::min(TAIL_GRID, std::max(1, std::atoi(e))) : 64;
       }();
       hipLaunchKernelGGL((tail_kernel<E_>), dim3(std::min(b->S, std::min(b->pdhg_grid, tail_grid))),
                          dim3(WAVE), tlds, b->stream, a, b->md, has_md);
@@ -3334,7 +3424,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, status,
                      iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa,
                      cached ? (const int32_t *)b->d_ctr : nullptr,
-                     cached ? (const int32_t *)b->d_wl2 : nullptr);
+                     cached ? (const int32_t *)b->d_wl2 : nullptr, b->d_err);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -3395,10 +3485,12 @@ int ph_batch_get_diag(ph_batch_t b, double *out) {
 int ph_batch_solve_summary(ph_batch_t b, int64_t *out) {
   if (!b || !out) return fail(PH_EINVAL, "ph_batch_solve_summary: bad arguments");
   unsigned long long h[5];
+  int32_t e[4];
   HIP_OK(hipMemcpyAsync(h, b->d_summary, sizeof(h), hipMemcpyDeviceToHost, b->stream));
+  if (int rc = queue_err_copy(b, e)) return rc;
   HIP_OK(hipStreamSynchronize(b->stream));
   for (int i = 0; i < 5; ++i) out[i] = (int64_t)h[i];
-  return PH_OK;
+  return check_dev(e);
 }
 
 int ph_loop_reset(ph_batch_t b, int32_t start_iter, int32_t iter_limit, double convthresh) {
@@ -3432,12 +3524,6 @@ int ph_loop_set_xbar(ph_batch_t b, const double *x, const double *prob_coeff, in
   }
   if (!x || !prob_coeff || !slot_k || !slot_s0 || !slot_s1 || !out_sums || !b->d_nonant_col)
     return fail(PH_EINVAL, "ph_loop_set_xbar: bad arguments");
-  if (b->mid) {  // one block per node slot (the chunked
-                 // form faulted on this path's graph replays)
-    b->loop_xa = XbarArgs{b->S, G, x, prob_coeff, b->d_nonant_col, slot_k, slot_s0, slot_s1, out_sums,
-                          0, nullptr, nullptr};
-    return PH_OK;
-  }
   // chunks of at most SUM_CHUNK scenarios per slot, their partials, a ticket
   const int C = std::max(1, (b->S + SUM_CHUNK - 1) / SUM_CHUNK);
   if ((size_t)2 * G * C > b->xpart_cap) {
@@ -3529,8 +3615,11 @@ int ph_loop_conv_local(ph_batch_t b, const double *absdiff, const int32_t *seg, 
 int ph_loop_status(ph_batch_t b, int64_t *out) {
   if (!b || !out) return fail(PH_EINVAL, "ph_loop_status: bad arguments");
   LoopCtl h;
+  int32_t e[4];
   HIP_OK(hipMemcpyAsync(&h, b->d_ctl, sizeof(h), hipMemcpyDeviceToHost, b->stream));
+  if (int rc = queue_err_copy(b, e)) return rc;
   HIP_OK(hipStreamSynchronize(b->stream));
+  if (int rc = check_dev(e)) return rc;
   out[0] = h.stop;
   out[1] = h.iter;
   out[2] = (int64_t)h.acc[0];
@@ -3602,8 +3691,10 @@ int ph_debug_prof(ph_batch_t b, int32_t on, int64_t *out) {
 
 int ph_batch_sync(ph_batch_t b) {
   if (!b) return fail(PH_EINVAL, "null batch");
+  int32_t e[4];
+  if (int rc = queue_err_copy(b, e)) return rc;
   HIP_OK(hipStreamSynchronize(b->stream));
-  return PH_OK;
+  return check_dev(e);
 }
 
 void ph_batch_destroy(ph_batch_t b) {
@@ -3613,7 +3704,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
-                  b->d_ctl, b->d_sym, b->d_ws, b->d_mlist, b->d_mctr,
+                  b->d_ctl, b->d_sym, b->d_ws, b->d_mlist, b->d_mctr, b->d_err,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

@@ -335,9 +335,17 @@ class PHBase(SPBase):
             name = type(self.spcomm).__name__
         why = {1: f"PDHG iteration limit ({max_iters}) reached before the KKT tolerance",
                2: "primal infeasible", 3: "dual infeasible (unbounded)"}
-        for i in np.nonzero(status != 0)[0]:
+        # the reference prints one line per failed solve (phbase.py:959-978);
+        # a batch of 10k scenarios prints the first few and a count (all of
+        # them with verbose)
+        bad = np.nonzero(status != 0)[0]
+        show = bad if self.PHoptions.get("verbose", False) else bad[:5]
+        for i in show:
             print(f"[{name}] Solve failed for scenario {self.local_scenario_names[i]}: "
                   f"{why.get(int(status[i]), 'status %d' % status[i])}")
+        if len(show) < len(bad):
+            print(f"[{name}] ... {len(bad) - len(show)} more failed solves "
+                  f"({len(bad)} of {self.S_loc} local scenarios)")
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -670,14 +678,10 @@ class PHBase(SPBase):
 
     def _graph_ok(self):
         """Replay chunks of the device loop as one HIP graph: a single GPU rank
-        (collectives stay eager) on a CUDA device, one-wave scenarios (n + m
-        <= 63).  Mid-size scenarios launch eagerly: their iterations take
-        milliseconds, so graphs save nothing there, and a graph-replayed
-        mid-size chunk faulted intermittently."""
+        (collectives stay eager) on a CUDA device."""
         b = self.batch
         return (self.PHoptions.get("device_loop_graphs", True) and self.comm.size == 1
-                and self.device.type == "cuda" and hasattr(b, "set_stream")
-                and b.n + b.m <= 63)
+                and self.device.type == "cuda" and hasattr(b, "set_stream"))
 
     def _capture_chunk(self, kw, chunk):
         """Capture `chunk` device iterations (the library's launches moved to

@@ -117,9 +117,9 @@ def test_lagrangian_bound_matches_oracle():
     assert abs(psb - opsb) / abs(opsb) < 1e-6
 
 
-@pytest.mark.parametrize("inst,S", [("sslp_15_45_5", 5), ("sslp_15_45_10", 10),
-                                    ("sslp_15_45_15", 15)])
-def test_sslp_lp_relaxation_ph_matches_oracle(inst, S):
+@pytest.mark.parametrize("inst,S,grid", [("sslp_15_45_5", 5, 0), ("sslp_15_45_10", 10, 2),
+                                         ("sslp_15_45_15", 15, 0), ("sslp_15_45_15", 15, 2)])
+def test_sslp_lp_relaxation_ph_matches_oracle(inst, S, grid, monkeypatch):
     """sslp_15_45_{5,10,15} LP relaxation (705 columns, 60 rows, ~1364
     nonzeros per scenario: the mid-size path, long rows summed by waves).  No
     reference pin exists for sslp (parity unpinned against the reference).
@@ -127,9 +127,14 @@ def test_sslp_lp_relaxation_ph_matches_oracle(inst, S):
     depends on the vertex a solver returns; checked against the oracle: the
     trivial bound (unique), then PH prox-QP solves from the oracle's own PH
     states (W, xbar after iterations 1 and 4), whose nonant optimum is
-    unique."""
+    unique.  grid > 0 caps the mid-size resident grid (PHGPU_MID_GRID) so
+    every block takes several scenarios through the phase kernels' work
+    queue (next_index) and reuses its polish workspace slice, as at 10k
+    scenarios."""
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import sslp
+    if grid:
+        monkeypatch.setenv("PHGPU_MID_GRID", str(grid))
     names = sslp.scenario_names(S)
     opts = _opts(PHIterLimit=10, defaultPHrho=1.0, convthresh=1e-6)
     ph = PH(dict(opts), names, sslp.scenario_creator,
@@ -363,8 +368,13 @@ def test_host_loop_device_loop_and_graphs_agree():
         assert abs(t - t0) <= 1e-9 * abs(t0)  # Iter0 LP dual objectives at 1e-9 KKT
         assert _rel(x, x0) < 1e-11
         # W sums 60 iterations of rho (x_s - xbar) over per-scenario x at
-        # 1e-9 relative KKT; elementwise (floor 1) it agrees to ~1e-8
-        assert _rel(w, w0) < 1e-7
+        # 1e-9 relative KKT; elementwise (floor 1) it agrees to ~1e-8.  The
+        # host and device loops run the same kernels but not bitwise the
+        # same sums: the host loop's Compute_Xbar is ph_xbar_accum (one block
+        # per node slot), the device loop's the post-solve kernel's chunked
+        # sums (SUM_CHUNK partials combined in chunk order), so x-bar differs
+        # in the last bits and the solves' 1e-9 KKT stop amplifies that
+        assert _rel(w, w0) < 5e-8
 
 
 def _gpu_rank_worker(rank, world, port, q, convthresh):
@@ -472,8 +482,19 @@ def test_hydro_ph_trajectory_from_oracle_iter0_point():
     assert abs(eobj - oe) <= 1e-5 * abs(oe)
 
 
-@pytest.mark.parametrize("iters", [6, 12])
-def test_farmer_c100_mid_path_matches_oracle(iters):
+_C100_ORACLE = {}
+
+
+def _c100_oracle(names, opts, iters):
+    """The oracle PH of the c=100 test case (cached across grid variants)."""
+    if iters not in _C100_ORACLE:
+        orc = OraclePH(dict(opts), [om.farmer(nm, 100) for nm in names])
+        _C100_ORACLE[iters] = (orc, orc.ph_main())
+    return _C100_ORACLE[iters]
+
+
+@pytest.mark.parametrize("iters,grid", [(6, 0), (12, 0), (6, 3), (12, 3)])
+def test_farmer_c100_mid_path_matches_oracle(iters, grid, monkeypatch):
     """BASELINE's HBM-regime scenario shape (farmer crops_multiplier 100:
     1200 columns, 901 rows, 2700 nonzeros, one 300-entry row) through the
     mid-size path (mid_kernel / mid_polish_kernel, 1024-thread blocks, the
@@ -481,18 +502,24 @@ def test_farmer_c100_mid_path_matches_oracle(iters):
     from scen3 (scen0-2 have identical yields across the crop copies, a
     non-unique Iter0 optimum), 6 and 12 PH iterations (12: past the point
     where, at 10k scenarios, the warm polish met degenerate vertices and
-    pins rows).  Trivial bound 1e-7, Eobj / x-bar / W 1e-5
-    elementwise, equal iteration count (phbase.py:1364-1566)."""
+    pins rows).  grid 3 caps the resident grid
+    (PHGPU_MID_GRID) so each block takes four scenarios through the phase
+    kernels' work queue (next_index) and its HBM polish workspace slice --
+    the code path F3 runs at 10k scenarios.  The device loop replays one
+    16-iteration HIP graph chunk, past the stop.  Trivial bound 1e-7, Eobj /
+    x-bar / W 1e-5 elementwise, equal iteration count
+    (phbase.py:1364-1566)."""
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
+    if grid:
+        monkeypatch.setenv("PHGPU_MID_GRID", str(grid))
     names = [f"scen{i}" for i in range(3, 15)]
     opts = _opts(PHIterLimit=iters, defaultPHrho=1.0, convthresh=1e-7)
     ph = PH(dict(opts), names, farmer.scenario_creator,
             scenario_creator_kwargs={"crops_multiplier": 100})
     conv, eobj, tb = ph.ph_main()
     assert ph.batch.S == 12 and ph.batch.n == 1200 and ph.batch.m == 901
-    orc = OraclePH(dict(opts), [om.farmer(nm, 100) for nm in names])
-    oc, oe, ot = orc.ph_main()
+    orc, (oc, oe, ot) = _c100_oracle(names, opts, iters)
     assert ph._PHIter == orc.iters
     assert abs(tb - ot) <= 1e-7 * abs(ot)
     assert abs(eobj - oe) <= 1e-5 * abs(oe)
@@ -565,3 +592,32 @@ def test_iteration_limit_gives_safe_outer_bound(c):
     orc = OraclePH(dict(opts), [om.farmer(nm, c) for nm in names])
     ot = orc.Iter0()
     assert bound <= ot + 1e-9 * abs(ot)
+
+
+def test_mid_path_graph_replay_matches_eager(monkeypatch):
+    """The mid-size path's device loop replayed as HIP graphs (16-iteration
+    chunks, the stop reached inside a chunk, every later kernel of the chunk
+    replayed against a stopped loop) computes what the eager device loop
+    computes, with a capped resident grid (every block takes several
+    scenarios through the work queue and reuses its workspace slice);
+    the device-side checks (list counts, entries, workspace slices) stay
+    clean (a violation raises PHGPUError at the loop's status read)."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    monkeypatch.setenv("PHGPU_MID_GRID", "3")
+    names = [f"scen{i}" for i in range(3, 15)]
+    res = []
+    for graphs in (False, True):
+        opts = _opts(PHIterLimit=21, defaultPHrho=1.0, convthresh=-1.0,
+                     device_loop_graphs=graphs)
+        ph = PH(dict(opts), names, farmer.scenario_creator,
+                scenario_creator_kwargs={"crops_multiplier": 100})
+        conv, eobj, tb = ph.ph_main()
+        assert bool(ph._loop_graphs) == graphs
+        res.append((ph._PHIter, conv, eobj, ph.xbar.cpu().numpy().copy(), ph.W.cpu().numpy().copy()))
+    (i0, c0, e0, x0, w0), (i1, c1, e1, x1, w1) = res
+    assert i0 == i1 == 21
+    assert abs(c1 - c0) <= 1e-12 * abs(c0)
+    assert abs(e1 - e0) <= 1e-12 * abs(e0)
+    assert _rel(x1, x0) < 1e-12
+    assert _rel(w1, w0) < 1e-12
