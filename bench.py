@@ -144,13 +144,24 @@ def cpu_baseline(c, scens, convthresh, cores=16, f3_crops=100, f3_sample=64, f3_
     return out
 
 
-def pmc_traffic(kname, S_loc, c):
+def workload_tag(kind, S_loc, c=None):
+    """The workload tag tools/pmc_summary.py writes into a PMC summary
+    (farmer10k_c1, farmer10k_c100, sslp10k), or None for a size no
+    committed profile describes."""
+    if S_loc != 10000:
+        return None
+    return f"farmer10k_c{c}" if kind == "farmer" else "sslp10k"
+
+
+def pmc_traffic(kname, tag):
     """HBM bytes per launch of `kname` from the committed rocprofv3 PMC passes
-    (profiles/r*/pmc_summary.json, written by tools/pmc_summary.py from
-    separate FETCH_SIZE / WRITE_SIZE passes of this bench command, gfx950
-    FETCH_SIZE x2 correction applied there), when they were collected on
-    this workload; else None."""
+    (profiles/r*/pmc_summary*.json, written by tools/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE passes of a bench command that ran only
+    this workload, gfx950 FETCH_SIZE x2 correction applied there), matched on
+    the summary's workload tag (the newest round first); else None."""
     import glob
+    if tag is None:
+        return None, None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary*.json")),
                        reverse=True):
         try:
@@ -159,7 +170,7 @@ def pmc_traffic(kname, S_loc, c):
         except (OSError, ValueError):
             continue
         k = d.get("kernels", {}).get(kname)
-        if k and d.get("scenarios_per_rank") == S_loc and d.get("crops_multiplier") == c:
+        if k and d.get("workload") == tag:
             return k.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
 
@@ -247,7 +258,8 @@ def hbm_config(args, world, farmer, PH, opts):
     stream_bytes = steps * bytes_per_pdhg_iter(c) + alg
     kern_ms = k_ms / max(nk, 1)
     tfs = (steps * pdhg_flops_per_step(c)) / (k_ms / nt / 1000.0) / 1e12 if k_ms > 0 else 0.0
-    trf = [pmc_traffic(k, ph.S_loc, c)[0] for k in ("mid_kernel", "mid_polish_kernel")]
+    trf = [pmc_traffic(k, workload_tag("farmer", ph.S_loc, c))[0]
+           for k in ("mid_kernel", "mid_polish_kernel")]
     traffic = None
     if all(t is not None for t in trf) and nk and np_:
         traffic = round(trf[0] * nk / nt + trf[1] * np_ / nt)   # HBM bytes per solve call
@@ -552,7 +564,7 @@ def run():
     mean_iters = tot_iters / max(n_solves, 1)
     polished_frac = n_polished / max(n_solves, 1)
     cached_frac = n_cached / max(n_solves, 1)
-    traffic, traffic_src = pmc_traffic(kname, S_loc, c)
+    traffic, traffic_src = pmc_traffic(kname, workload_tag("farmer", S_loc, c))
 
     # PH wall-clock to convergence tolerance (fresh runs, same instance): the
     # 10k headline size, and the CPU baseline's sample size beside it

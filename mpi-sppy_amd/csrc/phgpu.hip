@@ -389,7 +389,7 @@ struct SolveArgs {
   // the safe-bound pass take this list), or null
   int32_t *ul, *ul_count;
   const LoopCtl *ctl;  // device loop control or null
-  unsigned long long *prof;  // [16] phase clocks of the warm polish, or null
+  unsigned long long *prof;  // [PROF_SLOTS] debug clocks and counters (ph_debug_prof), or null
   int32_t *err;              // [4] device-side invariant checks (dev_fail)
 };
 
@@ -563,6 +563,88 @@ __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, WAVE));
   return v;
+}
+
+// ------------------------------------------------------------------------
+// Infeasibility certificates (PDLP-style).  On an infeasible or unbounded
+// subproblem the PDHG operator has no fixed point and the iterates drift
+// along its minimal displacement vector, so the trial point's displacement
+// from the Halpern anchor (since the last restart) is tested as
+//  - a dual ray y (rows; primal infeasibility, a Farkas certificate): y
+//    projected on the sign cone of the row bounds, dual ray objective
+//      sum_i [y>0] y rl_i + [y<0] y ru_i + sum_j min_{l<=x<=u} -(A'y)_j x_j
+//    > 0, a reduced cost -(A'y)_j that pushes towards an infinite column
+//    bound counting as a violation;
+//  - a primal ray d (columns; dual infeasibility, unboundedness): d
+//    projected on the recession cone of the column bounds (0 on a column
+//    with two finite bounds or a prox term), g'd < 0, A d in the recession
+//    cone of the row bounds up to the violations.
+// A ray is accepted when its objective is significant (> INFEAS_SIG times
+// the sum of its terms' magnitudes) and its violations are at most
+// INFEAS_EPS times the objective: for a feasible (bounded) problem weak
+// duality bounds the objective by violations x |a feasible point| (|a dual
+// feasible point|), so a false certificate would need entries of 1e8 in the
+// scaled space.  Tested from step INFEAS_MIN_IT on, every fourth KKT check
+// without a restart (two extra products per 4 x check_every steps).
+// ------------------------------------------------------------------------
+constexpr double INFEAS_EPS = 1e-8;
+constexpr double INFEAS_SIG = 1e-10;
+constexpr int INFEAS_MIN_IT = 256;
+
+__device__ __forceinline__ double ray_row_proj(double y, double RL, double RU) {
+  if (!isfinite(RL)) y = fmin(y, 0.0);
+  if (!isfinite(RU)) y = fmax(y, 0.0);
+  return y;
+}
+__device__ __forceinline__ double ray_col_proj(double d, double L, double U, double Q) {
+  const bool lf = isfinite(L), uf = isfinite(U);
+  if (Q > 0.0 || (lf && uf)) return 0.0;
+  if (lf) return fmax(d, 0.0);
+  if (uf) return fmin(d, 0.0);
+  return d;
+}
+// v[0] dual ray objective, v[1] its terms' magnitudes, v[2] its violations,
+// v[3] primal ray objective, v[4] its terms' magnitudes, v[5] its violations.
+// Row i: y = the projected dual ray entry, ad = (A d)_i of the primal ray.
+__device__ __forceinline__ void ray_terms_row(double y, double RL, double RU, double ad,
+                                              double (&v)[6]) {
+  const double t = y > 0.0 ? y * RL : (y < 0.0 ? y * RU : 0.0);
+  v[0] += t;
+  v[1] += fabs(t);
+  const bool lf = isfinite(RL), uf = isfinite(RU);
+  if (lf && uf) v[5] += fabs(ad);
+  else if (lf) v[5] += fmax(-ad, 0.0);
+  else if (uf) v[5] += fmax(ad, 0.0);
+}
+// Column j: aty = (A'y)_j of the dual ray, d = the projected primal ray entry.
+__device__ __forceinline__ void ray_terms_col(double aty, double L, double U, double G, double d,
+                                              double (&v)[6]) {
+  const double r = -aty;  // reduced cost of the homogeneous problem
+  if (r > 0.0) {
+    if (isfinite(L)) {
+      v[0] += r * L;
+      v[1] += fabs(r * L);
+    } else {
+      v[2] += r;
+    }
+  } else if (r < 0.0) {
+    if (isfinite(U)) {
+      v[0] += r * U;
+      v[1] += fabs(r * U);
+    } else {
+      v[2] -= r;
+    }
+  }
+  v[3] += G * d;
+  v[4] += fabs(G * d);
+}
+// The certified status of block-summed ray terms, or -1.
+__device__ __forceinline__ int ray_status(const double (&v)[6]) {
+  if (v[0] > 0.0 && v[0] > INFEAS_SIG * v[1] && v[2] <= INFEAS_EPS * v[0])
+    return PH_STATUS_PRIMAL_INFEASIBLE;
+  if (v[3] < 0.0 && -v[3] > INFEAS_SIG * v[4] && v[5] <= INFEAS_EPS * -v[3])
+    return PH_STATUS_DUAL_INFEASIBLE;
+  return -1;
 }
 
 struct ActiveSet {
@@ -1119,6 +1201,7 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
 
   double LAM[CPT];  // scaled reduced costs of the last KKT evaluation
   int how = 0;      // 0: PDHG reached tol, 1: polished at start, 2: polished mid-solve
+  int nchk = 0;     // KKT checks (the infeasibility test runs on every fourth)
 
   // Local KKT terms of the trial point (XN, YN, AXN), unscaled; ys must hold
   // YN.  v[0..5] = primal residual^2, dual residual^2, primal objective,
@@ -1370,6 +1453,41 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
       k = 0;
       r_restart = r;
     }
+    if (!restart && it >= INFEAS_MIN_IT && (++nchk & 3) == 0) {
+      // infeasibility certificates from the displacement since the anchor
+      double dd[CPT];
+      __syncthreads();  // every read of xs / ys of the check done
+#pragma unroll
+      for (int b = 0; b < RPT; ++b) {
+        int i = tid + b * T;
+        if (i < m) ys[i] = ray_row_proj(YN[b] - Z0Y[b], RL[b], RU[b]);
+      }
+#pragma unroll
+      for (int b = 0; b < CPT; ++b) {
+        int j = tid + b * T;
+        dd[b] = j < n ? ray_col_proj(XN[b] - Z0X[b], L[b], U[b], Q[b]) : 0.0;
+        if (j < n) xs[j] = dd[b];
+      }
+      __syncthreads();
+      double rv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      CL.dots(ys, part_c, DOT);
+#pragma unroll
+      for (int b = 0; b < CPT; ++b)
+        if (tid + b * T < n) ray_terms_col(DOT[b], L[b], U[b], G[b], dd[b], rv);
+      RW.dots(xs, part_r, DOT);
+#pragma unroll
+      for (int b = 0; b < RPT; ++b) {
+        int i = tid + b * T;
+        if (i < m) ray_terms_row(ys[i], RL[b], RU[b], DOT[b], rv);
+      }
+      block_sum<6>(rv, red);
+      const int cert = ray_status(rv);
+      if (cert >= 0) {
+        stat = cert;
+        ++it;
+        break;
+      }
+    }
     __syncthreads();  // all reads of ys (check col phase) done
 #pragma unroll
     for (int b = 0; b < RPT; ++b) {
@@ -1433,7 +1551,9 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
     a.status[s] = stat;
     a.iters[s] = it;
     a.pobj[s] = out_pobj;
-    a.dbound[s] = stat == PH_STATUS_OPTIMAL ? out_dobj : safe_bound;
+    // (an unbounded subproblem's outer bound is -inf)
+    a.dbound[s] = stat == PH_STATUS_OPTIMAL ? out_dobj
+                  : (stat == PH_STATUS_DUAL_INFEASIBLE ? -INFINITY : safe_bound);
     a.diag[PH_DIAG_W * s + 0] = d_ep;
     a.diag[PH_DIAG_W * s + 1] = d_ed;
     a.diag[PH_DIAG_W * s + 2] = d_eg;
@@ -3047,6 +3167,9 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
 // lists are empty in the PH steady state, so a small grid-strided grid.
 constexpr int TAIL_GRID = 512;
 
+// Slots of the debug counters (ph_debug_prof).
+constexpr int PROF_SLOTS = 32;
+
 // The repaired Lagrangian bound of the scenarios a solve left short of
 // the tolerance (bound_kernel; blocks of the others exit at once).
 // list == null: every scenario (grid S); else list[0 .. *count) with a
@@ -3667,21 +3790,21 @@ int ph_batch_read_timing(ph_batch_t b, double *out) {
 }
 
 // Debug (not in phgpu.h): phase clocks of pdhg_kernel's warm polish, in
-// 100 MHz ticks.  on != 0 clears and enables, on == 0 disables; read copies
-// out[16] {polishes, prologue, polish, GJ solves, GJ, cache store,
-// ok 1st attempt, ok 2nd attempt, failed}.
+// 100 MHz ticks, and exit-reason counters of the mid-size polish (slots in
+// solve_mid.inc).  on != 0 clears and enables, on == 0 disables; read copies
+// out[PROF_SLOTS].
 int ph_debug_prof(ph_batch_t b, int32_t on, int64_t *out) {
   if (!b) return fail(PH_EINVAL, "null batch");
   if (out && b->d_prof) {
-    HIP_OK(hipMemcpyAsync(out, b->d_prof, 16 * 8, hipMemcpyDeviceToHost, b->stream));
+    HIP_OK(hipMemcpyAsync(out, b->d_prof, PROF_SLOTS * 8, hipMemcpyDeviceToHost, b->stream));
     HIP_OK(hipStreamSynchronize(b->stream));
   }
   if (on) {
     if (!b->d_prof) {
-      int rc = dalloc(&b->d_prof, 16);
+      int rc = dalloc(&b->d_prof, PROF_SLOTS);
       if (rc) return rc;
     }
-    HIP_OK(hipMemsetAsync(b->d_prof, 0, 16 * 8, b->stream));
+    HIP_OK(hipMemsetAsync(b->d_prof, 0, PROF_SLOTS * 8, b->stream));
   } else if (!out && b->d_prof) {
     (void)hipFree(b->d_prof);
     b->d_prof = nullptr;

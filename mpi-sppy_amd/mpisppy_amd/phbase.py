@@ -317,14 +317,17 @@ class PHBase(SPBase):
 
     def _set_feasibility(self, nonopt, gripe, max_iters):
         """phbase.py:959-989: scenario_feasible from the per-scenario
-        statuses.  Only a solve that reached the KKT tolerance counts: a
-        scenario stopped at the PDHG iteration limit (status 1) holds an
-        iterate, not a solution, and reports a safe Lagrangian dual bound
-        (possibly -inf) as its outer bound; statuses 2/3 are certified
-        primal / dual infeasibility."""
+        statuses.  As in the reference, only a solve that ends infeasible or
+        unbounded makes the scenario infeasible: statuses 2 / 3 carry a
+        primal / dual infeasibility certificate (a Farkas ray of the PDHG
+        iterates, csrc/phgpu.hip ray_status).  A solve stopped at the PDHG
+        iteration limit (status 1, a solver's iteration limit in the
+        reference) keeps its iterate, is griped about, and reports a safe
+        Lagrangian dual bound (possibly -inf) as its outer bound; the xhat
+        inner bound requires status 0 (extensions/xhatbase.py)."""
         if nonopt:
             status = self.batch.status.cpu().numpy()
-            self.scenario_feasible = status == 0
+            self.scenario_feasible = status <= 1
         elif not self._all_feasible:
             self.scenario_feasible = np.ones(self.S_loc, dtype=bool)
         self._all_feasible = not nonopt
@@ -333,8 +336,9 @@ class PHBase(SPBase):
         name = type(self).__name__
         if self.spcomm is not None:
             name = type(self.spcomm).__name__
-        why = {1: f"PDHG iteration limit ({max_iters}) reached before the KKT tolerance",
-               2: "primal infeasible", 3: "dual infeasible (unbounded)"}
+        why = {1: f"PDHG iteration limit ({max_iters}) reached before the KKT tolerance "
+                  "(kept as feasible, safe outer bound)",
+               2: "primal infeasible (certificate)", 3: "dual infeasible, unbounded (certificate)"}
         # the reference prints one line per failed solve (phbase.py:959-978);
         # a batch of 10k scenarios prints the first few and a count (all of
         # them with verbose)

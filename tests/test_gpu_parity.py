@@ -551,14 +551,16 @@ def _farmer_with_infeasible(crops_multiplier):
 
 @pytest.mark.parametrize("c", [1, 10])
 def test_infeasible_scenario_stops_iter0(c):
-    """phbase.py:959-989 / 1415-1427: a scenario that is not solved to
-    tolerance (here infeasible: the iteration limit is reached) makes
-    scenario_feasible False and Iter0 stops; its outer bound is the safe
-    Lagrangian bound of its dual iterate (never above the optimum)."""
+    """phbase.py:959-989 / 1415-1427: an infeasible scenario (its cattle feed
+    cannot be met) is certified primal infeasible (status 2, a Farkas ray of
+    the PDHG iterates) long before the iteration limit, makes
+    scenario_feasible False and Iter0 stops.  c=1: the one-wave path
+    (pdhg_kernel), c=10: the mid-size path (mid_kernel)."""
     from mpisppy_amd.opt.ph import PH
     names = [f"scen{i}" for i in range(4)]
+    max_iters = 20000
     opts = _opts(PHIterLimit=3, per_scenario_models=True,
-                 iter0_solver_options={"pdhg_max_iters": 20000})
+                 iter0_solver_options={"pdhg_max_iters": max_iters})
     ph = PH(dict(opts), names, _farmer_with_infeasible(c),
             scenario_creator_kwargs={"crops_multiplier": c})
     ph.PH_Prep()
@@ -567,7 +569,47 @@ def test_infeasible_scenario_stops_iter0(c):
         ph.Iter0()
     assert list(ph.scenario_feasible) == [True, False, True, True]
     st = ph.batch.status.cpu().numpy()
-    assert st[1] != 0 and np.all(st[[0, 2, 3]] == 0)
+    assert st[1] == 2 and np.all(st[[0, 2, 3]] == 0)
+    assert ph.batch.iters.cpu().numpy()[1] <= max_iters // 10
+
+
+def _farmer_with_unbounded(crops_multiplier):
+    """farmer scenario creator whose scen2 is paid for buying crops (a
+    negative purchase price, purchases unbounded above): an unbounded LP."""
+    from mpisppy_amd.examples import farmer
+
+    def creator(name, **kw):
+        mdl = farmer.scenario_creator(name, **kw)
+        if name == "scen2":
+            sgn = 1.0 if mdl.sense == "min" else -1.0
+            for j in range(mdl.num_vars):
+                if "QuantityPurchased" in mdl._names[j]:
+                    mdl._obj.terms[j] = -1000.0 * sgn
+        return mdl
+    return creator
+
+
+@pytest.mark.parametrize("c", [1, 10])
+def test_unbounded_scenario_is_certified(c):
+    """An unbounded scenario subproblem gets status 3 (dual infeasible: a
+    primal ray of the PDHG iterates with negative cost) within a tenth of
+    the iteration limit and an outer bound of -inf; Iter0 stops on it as the
+    reference does on an unbounded termination (phbase.py:959-978)."""
+    from mpisppy_amd.opt.ph import PH
+    names = [f"scen{i}" for i in range(4)]
+    max_iters = 20000
+    opts = _opts(PHIterLimit=3, per_scenario_models=True,
+                 iter0_solver_options={"pdhg_max_iters": max_iters})
+    ph = PH(dict(opts), names, _farmer_with_unbounded(c),
+            scenario_creator_kwargs={"crops_multiplier": c})
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    with pytest.raises(RuntimeError, match="Infeasibility detected"):
+        ph.Iter0()
+    st = ph.batch.status.cpu().numpy()
+    assert st[2] == 3 and np.all(st[[0, 1, 3]] == 0)
+    assert ph.batch.iters.cpu().numpy()[2] <= max_iters // 10
+    assert ph.batch.dbound.cpu().numpy()[2] == -np.inf
 
 
 @pytest.mark.parametrize("c", [1, 10])
@@ -588,6 +630,9 @@ def test_iteration_limit_gives_safe_outer_bound(c):
     ph.solve_loop(solver_options=ph.current_solver_options, dis_W=True, dis_prox=True)
     st = ph.batch.status.cpu().numpy()
     assert np.any(st == 1)
+    # an iteration-limit solve stays feasible (the reference loads a limit
+    # solver's point, phbase.py:959-989) and carries the safe bound
+    assert np.all(ph.scenario_feasible)
     bound = ph.Ebound()
     orc = OraclePH(dict(opts), [om.farmer(nm, c) for nm in names])
     ot = orc.Iter0()
@@ -621,3 +666,41 @@ def test_mid_path_graph_replay_matches_eager(monkeypatch):
     assert abs(e1 - e0) <= 1e-12 * abs(e0)
     assert _rel(x1, x0) < 1e-12
     assert _rel(w1, w0) < 1e-12
+
+
+@pytest.mark.parametrize("device_loop", [True, False])
+def test_variable_probability_w_mask_matches_oracle(device_loop):
+    """spbase.py:369-400 / phbase.py:246-251 on the HIP path: per-variable
+    probabilities replace prob_coeff in Compute_Xbar and a zero-probability
+    nonant has its W masked (w_coeff) by update_w_conv_kernel (device loop)
+    or update_w_kernel (host loop).  Farmer S=12: slot 0 of the odd
+    scenarios at probability 0, of the even ones 2/S; W, x-bar, conv, Eobj
+    and the iteration count against the oracle."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    S = 12
+    names = [f"scen{i}" for i in range(S)]
+    probe = PH(_opts(), names, farmer.scenario_creator)
+    first = probe.nonant_names()[0]
+
+    def vprob(scen, first_name=None):
+        s = int(scen.name[4:])
+        return [(first_name, 2.0 / S if s % 2 == 0 else 0.0)]
+
+    opts = _opts(PHIterLimit=15, convthresh=1e-6, device_loop=device_loop,
+                 variable_probability_kwargs={"first_name": first},
+                 do_not_check_variable_probabilities=False)
+    ph = PH(dict(opts), names, farmer.scenario_creator, variable_probability=vprob)
+    conv, eobj, tb = ph.ph_main()
+    vp = {s: {0: (2.0 / S if s % 2 == 0 else 0.0)} for s in range(S)}
+    orc = OraclePH(dict(opts), [om.farmer(n) for n in names], variable_prob=vp)
+    oc, oe, ot = orc.ph_main()
+    assert ph._PHIter == orc.iters
+    W = ph.W.view(ph.K, ph.S_loc).cpu().numpy().T
+    assert np.all(W[1::2, 0] == 0.0) and np.any(W[0::2, 0] != 0.0)
+    assert _rel(W, np.array(orc.W)) < 1e-5
+    xb = ph.xbar.view(ph.K, ph.S_loc)[:, 0].cpu().numpy()
+    assert _rel(xb, orc.xbar[0]) < 1e-5
+    assert abs(conv - oc) <= 1e-3 * abs(oc)
+    assert abs(eobj - oe) <= 1e-5 * abs(oe)
+    assert abs(tb - ot) <= 1e-6 * abs(ot)

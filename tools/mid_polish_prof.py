@@ -26,7 +26,7 @@ b = ph.batch
 lib = b.lib
 lib.ph_debug_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
 lib.ph_debug_prof.restype = ctypes.c_int32
-out = np.zeros(16, dtype=np.int64)
+out = np.zeros(32, dtype=np.int64)
 lib.ph_debug_prof(b.handle, 1, None)
 b.set_timing(True)
 ph.run_device_loop(START, START + NIT, -1.0, chunk=NIT)
@@ -42,3 +42,5 @@ print(f"per polish (block-us): setup {us(out[15])/npol:.1f} factor {us(out[13])/
       f"solves {us(out[14])/npol:.1f}")
 print(f"rounds with a pinned row {out[5]}; exits: accepted {out[12]}, set repeats {out[1]}, non-finite {out[2]}, round limit {out[3]}; "
       f"failed checks: refinement short {out[4]}, ep {out[6]}, ed {out[7]}, eg {out[8]}")
+print(f"factorisations with a pivot held to its bound {out[16]}; non-finite: rhs {out[17]}, "
+      f"refinement solve {out[18]}, check only {out[19]}")

@@ -104,7 +104,7 @@ def run_f3(S=10000, c=100, nit=5):
     lib = b.lib
     lib.ph_debug_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
     lib.ph_debug_prof.restype = ctypes.c_int32
-    prof = np.zeros(16, dtype=np.int64)
+    prof = np.zeros(32, dtype=np.int64)
     for k in range(nit):
         lib.ph_debug_prof(b.handle, 1, None)
         torch.cuda.synchronize()

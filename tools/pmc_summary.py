@@ -1,6 +1,6 @@
 """Per-kernel HBM bytes per launch from rocprofv3 PMC passes of bench.py.
 
-    python tools/pmc_summary.py FETCH_DIR WRITE_DIR STATS_DIR OUT.json SCENS_PER_RANK CROPS [WINDOW]
+    python tools/pmc_summary.py FETCH_DIR WRITE_DIR STATS_DIR OUT.json WORKLOAD [WINDOW]
 
 FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
 output directories (separate passes, csv).  FETCH_SIZE and WRITE_SIZE are in
@@ -8,14 +8,27 @@ kB per dispatch; per MI355X_MICROARCH.md (HBM section) FETCH_SIZE on gfx950
 reports half the bytes of coalesced reads, so it is doubled here.
 STATS_DIR: the `--kernel-trace --stats` run (kernel time per launch).
 
+WORKLOAD names the one workload the profiled command ran (each profiled
+bench command runs ONE config: `--tol-run 0 --hbm-crops 0 --sslp-scens 0`
+for the farmer lines, `--crops 0 --hbm-crops 0 --sslp-scens N` style runs
+for sslp); the summary refuses a window whose kernel instances do not belong
+to it (a window that caught another config's launches is what mislabelled
+the round-2 profiles):
+
+  farmer10k_c1    active_set_kernel exactly once per solve, no mid-size kernel
+  farmer10k_c100  mid_kernel<1024, 2, 1> / mid_polish_kernel<1024, 2, 1> only
+                  (n = 1200, m = 901), no active_set_kernel
+  sslp10k         mid_kernel<1024, 1, 1> / mid_polish_kernel<1024, 1, 1> only
+                  (n = 705, m = 60)
+
 Window: the launches after the (WINDOW+1)-th last `summary_kernel` dispatch,
 i.e. the last WINDOW solve calls (one summary kernel closes each solve) --
-with --tol-run 0 and the F3 companion off (or on its own run) these are the
-eagerly launched PH iterations whose HIP-event times give the bench line's
-`achieved`, so traffic and algorithmic bytes describe the same launches.
-Kernels are named by their function name (template arguments dropped);
-`launches_per_solve` = launches in the window / WINDOW.  VGPR count and
-scratch (spill) bytes per lane come from the same records.
+the eagerly launched PH iterations whose HIP-event times give the bench
+line's `achieved`, so traffic and algorithmic bytes describe the same
+launches.  Kernels are named by their function name (template arguments
+dropped, kept under "instances"); `launches_per_solve` = launches in the
+window / WINDOW.  VGPR count and scratch (spill) bytes per lane come from
+the same records.
 """
 import csv
 import glob
@@ -25,6 +38,21 @@ import re
 import sys
 
 _NAME = re.compile(r"::(\w+)\s*[<(]")
+_INST = re.compile(r"::(\w+\s*<[^>]*>)")
+
+WORKLOADS = {
+    "farmer10k_c1": {"scenarios_per_rank": 10000, "crops_multiplier": 1,
+                     "require": {"active_set_kernel": None}, "forbid": ["mid_kernel", "mid_polish_kernel"],
+                     "once_per_solve": ["active_set_kernel"]},
+    "farmer10k_c100": {"scenarios_per_rank": 10000, "crops_multiplier": 100,
+                       "require": {"mid_kernel": "mid_kernel<1024, 2, 1>",
+                                   "mid_polish_kernel": "mid_polish_kernel<1024, 2, 1>"},
+                       "forbid": ["active_set_kernel"], "once_per_solve": []},
+    "sslp10k": {"scenarios_per_rank": 10000, "crops_multiplier": None,
+                "require": {"mid_kernel": "mid_kernel<1024, 1, 1>",
+                            "mid_polish_kernel": "mid_polish_kernel<1024, 1, 1>"},
+                "forbid": ["active_set_kernel"], "once_per_solve": []},
+}
 
 
 def short(name):
@@ -34,42 +62,70 @@ def short(name):
     return name.split("(")[0].strip()
 
 
+def instance(name):
+    m = _INST.search(name)
+    return m.group(1) if m else short(name)
+
+
 def _rows(d, pattern):
-    f = glob.glob(os.path.join(d, pattern))[0]
-    rows = list(csv.DictReader(open(f)))
+    f = glob.glob(os.path.join(d, "**", pattern), recursive=True)
+    if not f:
+        raise SystemExit(f"pmc_summary: no {pattern} under {d}")
+    rows = list(csv.DictReader(open(f[0])))
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     return rows
 
 
 def _window_start(rows, window):
     """Dispatch id after which the last `window` solve calls start."""
-    summ = [int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "summary_kernel"]
-    summ = sorted(set(summ))
+    summ = sorted({int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "summary_kernel"})
     if len(summ) <= window:
-        return -1
+        raise SystemExit(f"pmc_summary: only {len(summ)} solve calls recorded, window {window}")
     return summ[-window - 1]
 
 
 def per_kernel(d, counter, window):
     rows = [r for r in _rows(d, "*counter_collection.csv") if r["Counter_Name"] == counter]
     w0 = _window_start(rows, window)
-    vals, meta = {}, {}
+    vals, meta, inst = {}, {}, {}
     for r in rows:
         if int(r["Dispatch_Id"]) <= w0:
             continue
         k = short(r["Kernel_Name"])
         vals.setdefault(k, []).append(float(r["Counter_Value"]))
+        inst.setdefault(k, set()).add(instance(r["Kernel_Name"]))
         meta[k] = {"vgpr": int(r["VGPR_Count"]), "accum_vgpr": int(r["Accum_VGPR_Count"]),
                    "scratch_bytes_per_lane": int(r["Scratch_Size"]),
                    "lds_bytes": int(r["LDS_Block_Size"]), "workgroup": int(r["Workgroup_Size"])}
-    return {k: (sum(v) / len(v), len(v)) for k, v in vals.items()}, meta
+    return {k: (sum(v) / len(v), len(v)) for k, v in vals.items()}, meta, inst
+
+
+def validate(tag, res, inst):
+    """Refuse a window that holds another workload's kernels."""
+    w = WORKLOADS[tag]
+    ks = res["kernels"]
+    for k, want in w["require"].items():
+        if k not in ks:
+            raise SystemExit(f"pmc_summary: workload {tag} needs {k} in the window; found {sorted(ks)}")
+        if want is not None and inst.get(k) != {want}:
+            raise SystemExit(f"pmc_summary: workload {tag} needs only {want}; the window holds "
+                             f"{sorted(inst.get(k, []))}")
+    for k in w["forbid"]:
+        if k in ks:
+            raise SystemExit(f"pmc_summary: workload {tag}: {k} in the window belongs to another config")
+    for k in w["once_per_solve"]:
+        if ks[k]["launches_per_solve"] != 1.0:
+            raise SystemExit(f"pmc_summary: workload {tag}: {k} at {ks[k]['launches_per_solve']} "
+                             "launches per solve (a window of another config's solves)")
 
 
 def main():
-    fd, wd, sd, outp, spr, crops = sys.argv[1:7]
-    window = int(sys.argv[7]) if len(sys.argv) > 7 else 20
-    fetch, meta = per_kernel(fd, "FETCH_SIZE", window)
-    write, _ = per_kernel(wd, "WRITE_SIZE", window)
+    fd, wd, sd, outp, tag = sys.argv[1:6]
+    window = int(sys.argv[6]) if len(sys.argv) > 6 else 20
+    if tag not in WORKLOADS:
+        raise SystemExit(f"pmc_summary: unknown workload {tag}; one of {sorted(WORKLOADS)}")
+    fetch, meta, inst = per_kernel(fd, "FETCH_SIZE", window)
+    write, _, _ = per_kernel(wd, "WRITE_SIZE", window)
     trows = _rows(sd, "*kernel_trace.csv")
     w0 = _window_start(trows, window)
     times = {}
@@ -78,10 +134,12 @@ def main():
             continue
         times.setdefault(short(r["Kernel_Name"]), []).append(
             int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) + "
+    wl = WORKLOADS[tag]
+    res = {"workload": tag,
+           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) + "
                      "--kernel-trace --stats of the bench command",
            "fetch_correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section)",
-           "scenarios_per_rank": int(spr), "crops_multiplier": int(crops),
+           "scenarios_per_rank": wl["scenarios_per_rank"], "crops_multiplier": wl["crops_multiplier"],
            "window": f"launches of the last {window} solve calls (after the "
                      f"{window + 1}-th last summary_kernel dispatch)",
            "kernels": {}}
@@ -92,9 +150,11 @@ def main():
         hbm = None
         if fk is not None and wk is not None:
             hbm = round((2.0 * fk + wk) * 1024.0)
-        res["kernels"][k] = {"fetch_kB_raw": fk, "write_kB": wk, "hbm_bytes_per_launch": hbm,
+        res["kernels"][k] = {"instances": sorted(inst.get(k, [])),
+                             "fetch_kB_raw": fk, "write_kB": wk, "hbm_bytes_per_launch": hbm,
                              "launches_per_solve": round(nf / window, 3),
                              "mean_ns": (sum(t) / len(t)) if t else None, **meta.get(k, {})}
+    validate(tag, res, inst)
     with open(outp, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

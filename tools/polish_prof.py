@@ -25,7 +25,7 @@ b = ph.batch
 lib = b.lib
 lib.ph_debug_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
 lib.ph_debug_prof.restype = ctypes.c_int32
-out = np.zeros(16, dtype=np.int64)
+out = np.zeros(32, dtype=np.int64)
 lib.ph_debug_prof(b.handle, 1, None)
 b.set_timing(True)
 ph.run_device_loop(START, START + NIT, -1.0, chunk=NIT)
