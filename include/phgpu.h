@@ -275,6 +275,50 @@ int ph_loop_backup_status(ph_batch_t b, const int32_t *status, int32_t *status_s
 int ph_loop_status(ph_batch_t b, int64_t *out /*host [8]*/);
 
 /*
+ * One device-loop pass in one call (phbase.py:1498-1553, one iterk_loop
+ * iteration after its Compute_Xbar allreduce): the arguments are bound once
+ * per loop (ph_loop_bind_pass copies the struct; NULL unbinds), then every
+ * pass is ph_loop_pass(b), so the host issues one call per PH iteration
+ * (plus the collective on several ranks) instead of one per kernel.
+ *   conv_part == NULL (one rank): ph_loop_update_w_conv + ph_pdhg_solve.
+ *   conv_part != NULL (several ranks, the one-collective scheme above with
+ *     the convergence partials pre-weighted: conv = sum over ranks of
+ *     sum_s absdiff[s] * wconv[s], one slot): the lagged test of the
+ *     previous pass on *conv_part (allreduced by the caller together with
+ *     sums), this pass's Compute_Xbar broadcast + Update_W with its local
+ *     partial written to *conv_part, ph_loop_backup + ph_loop_backup_status
+ *     in one launch, ph_pdhg_solve.  After the loop the caller flushes the
+ *     last partial: allreduce + ph_loop_conv_lagged(conv_part, cnt = {1},
+ *     R = 1, nproc = 1).
+ * Replaces: the per-iteration body of PHBase.iterk_loop (phbase.py:1498-1553).
+ */
+typedef struct ph_loop_pass_args {
+  const double *sums;      /* dev [2G] node sums (allreduced on several ranks) */
+  int32_t G;
+  const int32_t *gid;      /* dev [K*S] */
+  const double *rho;       /* dev [K*S] */
+  const double *w_coeff;   /* dev [K*S] or NULL */
+  double *xbar;            /* dev [K*S] out */
+  double *xsqbar;          /* dev [K*S] out */
+  double *W;               /* dev [K*S] in-out */
+  double *absdiff;         /* dev [S] out */
+  const double *wconv;     /* dev [S] */
+  double *conv_hist;       /* dev [iter_limit] */
+  double *conv_part;       /* dev [1], several ranks; NULL on one rank */
+  double *x_save;          /* dev [n*S] (several ranks) */
+  double *y_save;          /* dev [m*S] (several ranks) */
+  int32_t *status_save;    /* dev [S] (several ranks) */
+  double *dbound_save;     /* dev [S] (several ranks) */
+  double w_on, prox_on;    /* the solve, as ph_pdhg_solve */
+  double *x, *y, *omega;
+  int32_t *status, *iters;
+  double *pobj, *dbound;
+  ph_solve_opts opts;
+} ph_loop_pass_args;
+int ph_loop_bind_pass(ph_batch_t b, const ph_loop_pass_args *args);
+int ph_loop_pass(ph_batch_t b);
+
+/*
  * Kernel timing of ph_pdhg_solve with HIP events recorded on the batch's
  * stream around its kernels of every solve while timing is on (set_timing
  * clears the record).  read_timing synchronises and returns out[8] =

@@ -1803,8 +1803,8 @@ __global__ void loop_conv_lagged_kernel(LoopCtl *c, const double *__restrict__ p
   if (c->stop == 1) return;
   const int k = c->pend;
   if (k > 0) {
-    double v = 0.0;
-    for (int r = 0; r < R; ++r) v += parts[r] / cnt[r];
+    double v = 0.0;  // (cnt == null: the partials carry their weights)
+    for (int r = 0; r < R; ++r) v += cnt ? parts[r] / cnt[r] : parts[r];
     v /= nproc;
     hist[k - 1] = v;
     c->pend = 0;
@@ -1847,6 +1847,24 @@ __global__ void __launch_bounds__(256) loop_backup_status_kernel(
     stb[s] = st[s];
     dbb[s] = db[s];
   }
+}
+
+// ph_loop_pass (several ranks): x, y, the statuses and the outer bounds
+// saved in one launch (the two kernels above), the pass marked pending.
+__global__ void __launch_bounds__(256) loop_backup_all_kernel(
+    LoopCtl *c, const double *__restrict__ x, double *__restrict__ xb, long nx,
+    const double *__restrict__ y, double *__restrict__ yb, long ny, const int32_t *__restrict__ st,
+    int32_t *__restrict__ stb, const double *__restrict__ db, double *__restrict__ dbb, int S) {
+  if (stopped(c)) return;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long i = i0; i < nx; i += stride) xb[i] = x[i];
+  for (long i = i0; i < ny; i += stride) yb[i] = y[i];
+  for (long i = i0; i < S; i += stride) {
+    stb[i] = st[i];
+    dbb[i] = db[i];
+  }
+  if (i0 == 0) c->pend = c->iter;
 }
 
 // Single-rank form: the per-reference-rank sums of absdiff over the
@@ -2539,7 +2557,8 @@ __global__ void __launch_bounds__(POST_BLOCK) update_w_conv_kernel(
     const double *__restrict__ rho, const double *__restrict__ wc,
     double *__restrict__ xbar, double *__restrict__ xsqbar, double *__restrict__ W,
     double *__restrict__ absdiff, const double *__restrict__ wconv, double *__restrict__ part,
-    int32_t *ticket, LoopCtl *ctl, double *__restrict__ hist, int32_t *ctr) {
+    int32_t *ticket, LoopCtl *ctl, double *__restrict__ hist, int32_t *ctr,
+    double *__restrict__ part_out) {
   __shared__ double red[MAX_WAVES];
   if (stopped(ctl)) return;
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2575,8 +2594,12 @@ __global__ void __launch_bounds__(POST_BLOCK) update_w_conv_kernel(
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    hist[ctl->iter - 1] = conv;
-    if (conv < ctl->thresh) ctl->stop = 1;
+    if (part_out) {  // several ranks: this rank's partial, tested one pass later
+      part_out[0] = conv;
+    } else {
+      hist[ctl->iter - 1] = conv;
+      if (conv < ctl->thresh) ctl->stop = 1;
+    }
     ctr[0] = 0;
     ctr[1] = 0;
     ctr[2] = 0;
@@ -2670,6 +2693,8 @@ struct ph_batch {
   int32_t *d_mlist = nullptr;  // [5][S] phase work lists
   int32_t *d_mctr = nullptr;   // [16] list counts (0..4) and queue counters (8..13)
   int32_t *d_err = nullptr;    // [4] device-side invariant checks (dev_fail)
+  ph_loop_pass_args pass{};    // ph_loop_bind_pass
+  bool pass_bound = false;
 };
 
 namespace {
@@ -3719,7 +3744,7 @@ int ph_loop_update_w_conv(ph_batch_t b, const double *x, const double *sums, int
     return fail(PH_EINVAL, "ph_loop_update_w_conv: reduction buffer too small");
   hipLaunchKernelGGL(update_w_conv_kernel, dim3(nb), dim3(POST_BLOCK), 0, b->stream, b->S, b->K, x,
                      b->d_nonant_col, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
-                     b->d_part, b->d_ctr + 4, b->d_ctl, conv_hist, b->d_ctr);
+                     b->d_part, b->d_ctr + 4, b->d_ctl, conv_hist, b->d_ctr, (double *)nullptr);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -3733,6 +3758,58 @@ int ph_loop_conv_local(ph_batch_t b, const double *absdiff, const int32_t *seg, 
                      seg, R, cnt, nproc, parts, conv_hist, b->d_ctr);
   HIP_OK(hipGetLastError());
   return PH_OK;
+}
+
+int ph_loop_bind_pass(ph_batch_t b, const ph_loop_pass_args *args) {
+  if (!b) return fail(PH_EINVAL, "null batch");
+  if (!args) {
+    b->pass_bound = false;
+    return PH_OK;
+  }
+  const ph_loop_pass_args &p = *args;
+  if (!p.sums || p.G <= 0 || !p.gid || !p.rho || !p.xbar || !p.xsqbar || !p.W || !p.absdiff ||
+      !p.wconv || !p.conv_hist || !p.x || (b->m && !p.y) || !p.omega || !p.status || !p.iters ||
+      !p.pobj || !p.dbound)
+    return fail(PH_EINVAL, "ph_loop_bind_pass: null argument");
+  if (p.conv_part && (!p.x_save || (b->m && !p.y_save) || !p.status_save || !p.dbound_save))
+    return fail(PH_EINVAL, "ph_loop_bind_pass: several ranks need the x/y/status/dbound saves");
+  if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_loop_bind_pass: no nonants declared");
+  b->pass = p;
+  b->pass_bound = true;
+  return PH_OK;
+}
+
+int ph_loop_pass(ph_batch_t b) {
+  if (!b || !b->loop_on || !b->pass_bound)
+    return fail(PH_EINVAL, "ph_loop_pass: loop not enabled or no pass bound");
+  const ph_loop_pass_args &p = b->pass;
+  const int nb = (b->S + POST_BLOCK - 1) / POST_BLOCK;
+  if ((size_t)nb > b->part_cap) return fail(PH_EINVAL, "ph_loop_pass: reduction buffer too small");
+  if (p.conv_part) {
+    // several ranks: the previous pass's convergence test on its allreduced
+    // partial (one pass late), then this pass's partial into the same slot
+    hipLaunchKernelGGL(loop_conv_lagged_kernel, dim3(1), dim3(1), 0, b->stream, b->d_ctl,
+                       (const double *)p.conv_part, (const double *)nullptr, 1, 1.0, p.conv_hist,
+                       b->d_ctr);
+    HIP_OK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(update_w_conv_kernel, dim3(nb), dim3(POST_BLOCK), 0, b->stream, b->S, b->K,
+                     (const double *)p.x, b->d_nonant_col, p.sums, p.G, p.gid, p.rho, p.w_coeff,
+                     p.xbar, p.xsqbar, p.W, p.absdiff, p.wconv, b->d_part, b->d_ctr + 4, b->d_ctl,
+                     p.conv_hist, b->d_ctr, p.conv_part);
+  HIP_OK(hipGetLastError());
+  if (p.conv_part) {
+    const long nx = (long)b->n * b->S, ny = b->m ? (long)b->m * b->S : 0;
+    const long mx = std::max(std::max(nx, ny), (long)b->S);
+    const int grid = (int)std::min<long>(std::max<long>((mx + 255) / 256, 1), 2048);
+    hipLaunchKernelGGL(loop_backup_all_kernel, dim3(grid), dim3(256), 0, b->stream, b->d_ctl,
+                       (const double *)p.x, p.x_save, nx, (const double *)p.y, p.y_save, ny,
+                       (const int32_t *)p.status, p.status_save, (const double *)p.dbound,
+                       p.dbound_save, b->S);
+    HIP_OK(hipGetLastError());
+  }
+  return ph_pdhg_solve(b, p.W, p.rho, p.xbar, p.w_on, p.prox_on, p.x, p.y, p.omega, p.status,
+                       p.iters, p.pobj, p.dbound, &p.opts);
 }
 
 int ph_loop_status(ph_batch_t b, int64_t *out) {

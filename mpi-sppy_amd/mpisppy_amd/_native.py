@@ -29,6 +29,18 @@ class SolveOpts(ctypes.Structure):
 DIAG_W = 5  # PH_DIAG_W in include/phgpu.h
 
 
+class LoopPassArgs(ctypes.Structure):
+    """ph_loop_pass_args of include/phgpu.h (field order and types exact)."""
+    _fields_ = [("sums", _c_ptr), ("G", _c_int), ("gid", _c_ptr), ("rho", _c_ptr),
+                ("w_coeff", _c_ptr), ("xbar", _c_ptr), ("xsqbar", _c_ptr), ("W", _c_ptr),
+                ("absdiff", _c_ptr), ("wconv", _c_ptr), ("conv_hist", _c_ptr),
+                ("conv_part", _c_ptr), ("x_save", _c_ptr), ("y_save", _c_ptr),
+                ("status_save", _c_ptr), ("dbound_save", _c_ptr), ("w_on", _c_dbl),
+                ("prox_on", _c_dbl), ("x", _c_ptr), ("y", _c_ptr), ("omega", _c_ptr),
+                ("status", _c_ptr), ("iters", _c_ptr), ("pobj", _c_ptr), ("dbound", _c_ptr),
+                ("opts", SolveOpts)]
+
+
 # (name, restype, argtypes) -- must match include/phgpu.h exactly
 SIGNATURES = [
     ("ph_version", ctypes.c_char_p, []),
@@ -62,6 +74,8 @@ SIGNATURES = [
                                 ctypes.c_int64]),
     ("ph_loop_backup_status", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
     ("ph_loop_status", _c_int, [_c_ptr, _c_ptr]),
+    ("ph_loop_bind_pass", _c_int, [_c_ptr, ctypes.POINTER(LoopPassArgs)]),
+    ("ph_loop_pass", _c_int, [_c_ptr]),
     ("ph_batch_set_timing", _c_int, [_c_ptr, _c_int]),
     ("ph_batch_read_timing", _c_int, [_c_ptr, _c_ptr]),
     ("ph_batch_sync", _c_int, [_c_ptr]),

@@ -321,6 +321,31 @@ class DeviceBatch:
                                                      _native.ptr(dbound_save)),
                       "ph_loop_backup_status")
 
+    def loop_bind_pass(self, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
+                       conv_hist, conv_part, saves, w_on, prox_on, tol=1e-9,
+                       max_iters=200000, check_every=64, warm_start=True, reflection=1.0,
+                       polish=True):
+        """Bind the arguments of ph_loop_pass for this loop (see phgpu.h);
+        conv_part / saves = (x_save, y_save, status_save, dbound_save) on
+        several ranks, None on one."""
+        P = _native.ptr
+        xs, ys, ss, ds = saves if saves is not None else (None, None, None, None)
+        a = _native.LoopPassArgs(
+            P(sums), int(G), P(gid), P(rho), P(w_coeff), P(xbar), P(xsqbar), P(W), P(absdiff),
+            P(wconv), P(conv_hist), P(conv_part), P(xs), P(ys), P(ss), P(ds), float(w_on),
+            float(prox_on), P(self.x), P(self.y), P(self.omega), P(self.status), P(self.iters),
+            P(self.pobj), P(self.dbound),
+            _native.SolveOpts(float(tol), int(max_iters), int(check_every),
+                              1 if warm_start else 0, float(reflection), 1 if polish else 0))
+        _native.check(self.lib.ph_loop_bind_pass(self.handle, ctypes.byref(a)), "ph_loop_bind_pass")
+
+    def loop_unbind_pass(self):
+        _native.check(self.lib.ph_loop_bind_pass(self.handle, None), "ph_loop_bind_pass")
+
+    def loop_pass(self):
+        """One device-loop pass (ph_loop_pass): one call per PH iteration."""
+        _native.check(self.lib.ph_loop_pass(self.handle), "ph_loop_pass")
+
     def loop_status(self):
         """(stop, iter, not-optimal solves, solves, PDHG iters sum, max, polished,
         cached); synchronises.  stop: 0 running, 1 converged, 2 iteration limit."""

@@ -114,6 +114,11 @@ class PHBase(SPBase):
         self.xconv = torch.zeros(2 * self.G + R, **f64)
         self.xsums = self.xconv[:2 * self.G]
         self.conv_parts = self.xconv[2 * self.G:]
+        # the device loop's pass (ph_loop_pass) allreduces [2G sums | one
+        # pre-weighted conv partial]
+        self.xpass = self.xconv[:2 * self.G + 1]
+        self.conv_part = self.xconv[2 * self.G:2 * self.G + 1]
+        self._one = torch.ones(1, **f64)
         self._x_save = self._y_save = None
         self.conv_cnt_dev = torch.as_tensor(self.conv_cnt, **f64)
         # the same weights per local scenario, 1/cnt[r(s)]/R (fused W + conv)
@@ -577,34 +582,35 @@ class PHBase(SPBase):
 
     def _device_iteration(self, kw):
         """One iterk_loop pass queued on the device (phbase.py:1498-1553 order):
-        Compute_Xbar -> Update_W -> convergence_diff -> [stop?] -> solve.
+        Compute_Xbar -> Update_W -> convergence_diff -> [stop?] -> solve, as
+        ONE library call (ph_loop_pass, bound by run_device_loop).
         Compute_Xbar's local sums of this pass were computed by the previous
         pass's post-solve kernel (or before the first pass); Compute_Xbar's
-        broadcast and Update_W are one kernel (update_w with W), which writes
-        what the two reference calls write."""
+        broadcast and Update_W are one kernel, which writes what the two
+        reference calls write.  Several ranks: one collective per pass
+        before it carries this pass's node sums and the previous pass's
+        (pre-weighted) convergence partial; the previous pass's convergence
+        test runs inside the call and, if it stops, the host restores the
+        x/y saved before that pass's solve (run_device_loop)."""
+        if self.comm.size > 1:
+            self._allreduce(self.xpass)
+        self.batch.loop_pass()
+
+    def _bind_pass(self, kw):
+        """ph_loop_bind_pass: the device loop's per-pass arguments, once."""
         b = self.batch
-        if self.comm.size == 1:  # one kernel: broadcast, Update_W, convergence_diff
-            b.loop_update_w_conv(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
-                                 self.xsqbar, self.W, self.absdiff, self.conv_w, self.conv_hist)
-        else:
-            # one collective per pass: this pass's xbar sums and the previous
-            # pass's conv partials; the previous pass's convergence test runs
-            # now and, if it stops, the host restores the x/y saved before
-            # that pass's solve (run_device_loop)
-            self._allreduce(self.xconv)
-            b.loop_conv_lagged(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc,
-                               self.conv_hist)
-            b.update_w(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
-                       self.xsqbar, self.W, self.absdiff)
-            b.segment_sum(self.absdiff, None, self.conv_seg, self.conv_parts)
+        saves = None
+        if self.comm.size > 1:
             if self._x_save is None:
                 self._x_save = torch.empty_like(b.x)
                 self._y_save = torch.empty_like(b.y)
                 self._st_save = torch.empty_like(b.status)
                 self._db_save = torch.empty_like(b.dbound)
-            b.loop_backup(self._x_save, self._y_save)
-            b.loop_backup_status(self._st_save, self._db_save)
-        b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
+            saves = (self._x_save, self._y_save, self._st_save, self._db_save)
+        b.loop_bind_pass(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
+                         self.xsqbar, self.W, self.absdiff, self.conv_w, self.conv_hist,
+                         self.conv_part if self.comm.size > 1 else None, saves,
+                         self.w_on, self.prox_on, **kw)
 
     def run_device_loop(self, start_iter, iter_limit, convthresh, chunk=None):
         """Run iterk_loop passes start_iter+1 .. iter_limit on the device,
@@ -625,6 +631,7 @@ class PHBase(SPBase):
         b.loop_reset(start_iter, iter_limit, convthresh)
         b.loop_enable(True)
         b.loop_set_xbar(self.prob_coeff, self.slot_k, self.slot_s0, self.slot_s1, self.xsums)
+        self._bind_pass(kw)
         # Compute_Xbar's local sums for the first pass
         b.xbar_accum(self.prob_coeff, self.slot_k, self.slot_s0, self.slot_s1, self.xsums)
         graph = None
@@ -654,12 +661,11 @@ class PHBase(SPBase):
                 if stop:
                     break
             if self.comm.size > 1:
-                # the last pass's conv partials (limit reached), then the
+                # the last pass's conv partial (limit reached), then the
                 # reference's state at a convergence break: x/y of before the
                 # solve that the lagged test showed should not have run
-                self._allreduce(self.conv_parts)
-                b.loop_conv_lagged(self.conv_parts, self.conv_cnt_dev, self.ref_n_proc,
-                                   self.conv_hist)
+                self._allreduce(self.conv_part)
+                b.loop_conv_lagged(self.conv_part, self._one, 1.0, self.conv_hist)
                 st = b.loop_status()
                 stop, it = st[0], st[1]
                 nonopt = nonopt or st[2]
@@ -676,6 +682,7 @@ class PHBase(SPBase):
         finally:
             b.loop_enable(False)
             b.loop_set_xbar(None, None, None, None, None)
+            b.loop_unbind_pass()
             self._loop_prev = (0, 0)
         self._set_feasibility(nonopt, True, kw["max_iters"])
         return stop, it

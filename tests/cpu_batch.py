@@ -97,7 +97,7 @@ class CPUBatch:
         if k > 0:
             v = 0.0
             for r in range(parts.numel()):
-                v += float(parts[r]) / float(cnt[r])
+                v += float(parts[r]) / (float(cnt[r]) if cnt is not None else 1.0)
             v /= nproc
             conv_hist[k - 1] = v
             c["pend"] = 0
@@ -117,6 +117,35 @@ class CPUBatch:
             return
         status_save.copy_(self.status)
         dbound_save.copy_(self.dbound)
+
+    _pass = None
+
+    def loop_bind_pass(self, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
+                       conv_hist, conv_part, saves, w_on, prox_on, **kw):
+        self._pass = dict(sums=sums, G=G, gid=gid, rho=rho, w_coeff=w_coeff, xbar=xbar,
+                          xsqbar=xsqbar, W=W, absdiff=absdiff, wconv=wconv, conv_hist=conv_hist,
+                          conv_part=conv_part, saves=saves, w_on=w_on, prox_on=prox_on)
+
+    def loop_unbind_pass(self):
+        self._pass = None
+
+    def loop_pass(self):
+        """ph_loop_pass semantics (include/phgpu.h)."""
+        p = self._pass
+        if p["conv_part"] is None:
+            self.loop_update_w_conv(p["sums"], p["G"], p["gid"], p["rho"], p["w_coeff"],
+                                    p["xbar"], p["xsqbar"], p["W"], p["absdiff"], p["wconv"],
+                                    p["conv_hist"])
+        else:
+            self.loop_conv_lagged(p["conv_part"], None, 1.0, p["conv_hist"])
+            if not self._stopped():
+                self.update_w(p["sums"], p["G"], p["gid"], p["rho"], p["w_coeff"], p["xbar"],
+                              p["xsqbar"], p["W"], p["absdiff"])
+                p["conv_part"][0] = float((p["absdiff"] * p["wconv"]).sum())
+                xs, ys, ss, ds = p["saves"]
+                self.loop_backup(xs, ys)
+                self.loop_backup_status(ss, ds)
+        self.solve(p["W"], p["rho"], p["xbar"], p["w_on"], p["prox_on"])
 
     def loop_status(self):
         c = self._ctl

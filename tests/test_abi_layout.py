@@ -149,3 +149,30 @@ def test_sslp_layout_matches_oracle(inst):
     # data_dir form of the reference's scenario_creator (sslp.py:17-25)
     m = sslp.scenario_creator("Scenario1", data_dir=f"data/{inst}/scenariodata")
     assert m.num_vars == bd.n
+
+
+def test_ctypes_structs_match_the_header_layout(tmp_path):
+    """The ctypes mirrors of ph_solve_opts and ph_loop_pass_args have the C
+    compiler's size and field offsets (gcc on include/phgpu.h)."""
+    import shutil
+    import subprocess
+    from mpisppy_amd import _native
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    structs = {"ph_solve_opts": _native.SolveOpts, "ph_loop_pass_args": _native.LoopPassArgs}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "phgpu.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'  printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {(a, b): int(c) for a, b, c in (ln.split() for ln in out if ln)}
+    for cname, cls in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(cls), cname
+        for fname, _ in cls._fields_:
+            assert got[(cname, fname)] == getattr(cls, fname).offset, (cname, fname)
