@@ -424,6 +424,9 @@ def _parser():
     ap.add_argument("--hbm-crops", type=int, default=100,
                     help="crops_multiplier of the HBM-bound companion config (F3); 0 = skip")
     ap.add_argument("--hbm-steps", type=int, default=5)
+    ap.add_argument("--graphs", type=int, default=1,
+                    help="replay the timed device-loop chunk as a HIP graph (0: eager launches, "
+                         "one ph_loop_pass call per PH iteration)")
     ap.add_argument("--sslp-scens", type=int, default=10000,
                     help="scenarios per rank of the sslp companion config (BASELINE config 5); 0 = skip")
     return ap
@@ -474,7 +477,8 @@ def run():
     opts = {"solvername": "mi355x_pdhg", "PHIterLimit": args.warmup + args.steps,
             "defaultPHrho": args.rho, "convthresh": -1.0, "verbose": False,
             "display_progress": False, "display_timing": False,
-            "iter0_solver_options": {}, "iterk_solver_options": {}}
+            "iter0_solver_options": {}, "iterk_solver_options": {},
+            "device_loop_graphs": bool(args.graphs)}
     _progress(f"building {S} scenarios (crops_multiplier {c})")
     ph = PH(opts, names, farmer.scenario_creator,
             scenario_creator_kwargs={"crops_multiplier": c})
@@ -525,7 +529,7 @@ def run():
     n_t, as_ms, po_ms, pd_ms, nk, k_ms, np_, p_ms = b.read_timing_full()
     sb_ = b.loop_status()
     b.set_timing(False)
-    ph.PHoptions["device_loop_graphs"] = True
+    ph.PHoptions["device_loop_graphs"] = bool(args.graphs)
     nt = max(n_t, 1)
     as_ms, po_ms, pd_ms = as_ms / nt, po_ms / nt, pd_ms / nt
     mid = (nk + np_) > 0      # a mid-size batch (--crops >= 6): its phase kernels instead

@@ -527,7 +527,14 @@ __device__ __forceinline__ void kkt_terms_row(double AXN, double YN, double RL, 
   const double axu = AXN * idr;
   const double rlu = RL * idr, ruu = RU * idr;
   const double rp = axu - clampd(axu, rlu, ruu);
-  const double yu = YN * DR;
+  double yu = YN * DR;
+  // a multiplier on the wrong side of a one-sided row (the LDL' polish's
+  // pinned estimates can be) is a dual infeasibility: counted in the dual
+  // residual instead of an infinite dual objective (whose gap is NaN)
+  if ((yu > 0.0 && !isfinite(rlu)) || (yu < 0.0 && !isfinite(ruu))) {
+    v[1] += yu * yu;
+    yu = 0.0;
+  }
   v[0] += rp * rp;
   v[3] += (yu > 0.0 ? yu * rlu : 0.0) + (yu < 0.0 ? yu * ruu : 0.0);
   if (isfinite(rlu)) v[4] += rlu * rlu;
@@ -1901,6 +1908,7 @@ __global__ void __launch_bounds__(1024) loop_conv_local_kernel(
 }
 
 #include "solve_mid.inc"
+#include "solve_big.inc"
 
 // ------------------------------------------------------------------------
 // polish_kernel: the misses of the active-set cache (work list wl), one
@@ -2695,6 +2703,13 @@ struct ph_batch {
   int32_t *d_err = nullptr;    // [4] device-side invariant checks (dev_fail)
   ph_loop_pass_args pass{};    // ph_loop_bind_pass
   bool pass_bound = false;
+  // big path (max(n, m) > 3072, solve_big.inc): the HBM-streaming kernels
+  bool big = false;
+  BigArgs bg{};
+  double *d_vals_t = nullptr;   // [S][nnz] CSC-ordered scaled values
+  double *d_bws = nullptr;      // workspace slices
+  size_t big_lds_bytes = 0;     // LDS of big_kernel (y + scratch)
+  int big_grid = 0;             // resident blocks of the big phase kernels
 };
 
 namespace {
@@ -2864,41 +2879,10 @@ static int check_dev(const int32_t (&e)[4]) {
   return fail(PH_EDEV, msg);
 }
 
-// Symbolic analysis of the KKT pattern, the tails of long lines and the
-// LDS plan of the mid-size path; uploads the index arrays (one buffer).
-static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx,
-                     const std::vector<int32_t> &col_ptr) {
-  if (!pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr))
-    return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns; the "
-                           "on-chip solver does not cover it");
-  if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx))
-    return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
-                               (b->sym.error ? b->sym.error : "?"));
-  const KktSymbolic &y = b->sym;
-  std::vector<int32_t> rwp, rtb, rln, rbb, rtp, cwp, ctb, cln, cbb, ctp;
-  build_tails(b->m, row_ptr, b->mblock, rwp, rtb, rln, rbb, rtp);
-  build_tails(b->n, col_ptr.data(), b->mblock, cwp, ctb, cln, cbb, ctp);
-  std::vector<const std::vector<int32_t> *> parts = {
-      &y.pos, &y.Lcp, &y.Lri, &y.Lcl, &y.Lrp, &y.Lrc, &y.Lrq, &y.lvp, &y.lvc, &y.lep, &y.lee,
-      &y.ecp, &y.ec1, &y.ec2, &y.eck, &y.apos, &y.arow,
-      &rwp, &rtb, &rln, &rbb, &rtp, &cwp, &ctb, &cln, &cbb, &ctp};
-  std::vector<size_t> off;
-  std::vector<int32_t> all;
-  for (auto *v : parts) {
-    off.push_back(all.size());
-    all.insert(all.end(), v->begin(), v->end());
-    all.resize((all.size() + 3) & ~size_t(3), 0);
-  }
-  int rc = dalloc(&b->d_sym, all.size());
-  if (rc) return rc;
-  HIP_OK(hipMemcpy(b->d_sym, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  const int32_t *d = b->d_sym;
-  int q = 0;
-  KktDev &kd = b->md.kd;
-  kd.N = y.N;
-  kd.nnzL = y.nnzL;
-  kd.NL = y.NL;
-  kd.chain0 = y.chain0;
+// The LDL' polish's knobs (measurement hooks, environment variables read
+// at batch creation): regularisation, PDAS rounds, pinned rows, refinement
+// tolerance.
+static int kkt_knobs(ph_batch *b) {
   {  // PHGPU_KKT_DELTA: measurement hook for the polish regularisation
     const char *e = std::getenv("PHGPU_KKT_DELTA");
     b->md.delta = e ? std::atof(e) : KKT_DELTA;
@@ -2924,6 +2908,66 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_refine_tol), &t, sizeof(t)));
     }
   }
+  return PH_OK;
+}
+
+// Symbolic analysis of the KKT pattern, the tails of long lines and the
+// LDS plan of the mid-size path; uploads the index arrays (one buffer).
+static int big_init(ph_batch *b);
+
+// Scenarios beyond the mid-size plan (max(n, m) > 3072) take the big path
+// (solve_big.inc): the same analysis, long-line lists instead of tails, the
+// state in HBM workspace slices.
+static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx,
+                     const std::vector<int32_t> &col_ptr) {
+  const bool big = !pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr);
+  if (big) {
+    b->mblock = BIG_BLOCK;
+    b->mpc = b->mpr = 0;
+  }
+  if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx))
+    return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
+                               (b->sym.error ? b->sym.error : "?"));
+  const KktSymbolic &y = b->sym;
+  std::vector<int32_t> rwp, rtb, rln, rbb, rtp, cwp, ctb, cln, cbb, ctp;
+  std::vector<int32_t> rlong(b->m, 0), clong(b->n, 0), lr, lc;
+  if (!big) {
+    build_tails(b->m, row_ptr, b->mblock, rwp, rtb, rln, rbb, rtp);
+    build_tails(b->n, col_ptr.data(), b->mblock, cwp, ctb, cln, cbb, ctp);
+  } else {
+    for (int i = 0; i < b->m; ++i)
+      if (row_ptr[i + 1] - row_ptr[i] > BIG_LONG) {
+        rlong[i] = 1;
+        lr.push_back(i);
+      }
+    for (int j = 0; j < b->n; ++j)
+      if (col_ptr[j + 1] - col_ptr[j] > BIG_LONG) {
+        clong[j] = 1;
+        lc.push_back(j);
+      }
+  }
+  std::vector<const std::vector<int32_t> *> parts = {
+      &y.pos, &y.Lcp, &y.Lri, &y.Lcl, &y.Lrp, &y.Lrc, &y.Lrq, &y.lvp, &y.lvc, &y.lep, &y.lee,
+      &y.ecp, &y.ec1, &y.ec2, &y.eck, &y.apos, &y.arow,
+      &rwp, &rtb, &rln, &rbb, &rtp, &cwp, &ctb, &cln, &cbb, &ctp, &rlong, &clong, &lr, &lc};
+  std::vector<size_t> off;
+  std::vector<int32_t> all;
+  for (auto *v : parts) {
+    off.push_back(all.size());
+    all.insert(all.end(), v->begin(), v->end());
+    all.resize((all.size() + 3) & ~size_t(3), 0);
+  }
+  int rc = dalloc(&b->d_sym, all.size());
+  if (rc) return rc;
+  HIP_OK(hipMemcpy(b->d_sym, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  const int32_t *d = b->d_sym;
+  int q = 0;
+  KktDev &kd = b->md.kd;
+  kd.N = y.N;
+  kd.nnzL = y.nnzL;
+  kd.NL = y.NL;
+  kd.chain0 = y.chain0;
+  if (int rc = kkt_knobs(b)) return rc;
   kd.pos = d + off[q++]; kd.Lcp = d + off[q++]; kd.Lri = d + off[q++]; kd.Lcl = d + off[q++];
   kd.Lrp = d + off[q++]; kd.Lrc = d + off[q++]; kd.Lrq = d + off[q++];
   kd.lvp = d + off[q++]; kd.lvc = d + off[q++]; kd.lep = d + off[q++]; kd.lee = d + off[q++];
@@ -2936,9 +2980,28 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   tc.ntail = (int)ctp.size();
   tc.wp = d + off[q++]; tc.tb = d + off[q++]; tc.ln = d + off[q++]; tc.b = d + off[q++];
   tc.tpos = d + off[q++];
-  // LDS plan (doubles): see the carve at the top of solve_mid
   auto up2 = [](long v) { return (v + 1) & ~1L; };
   auto up4 = [](long v) { return (v + 3) & ~3L; };
+  if (big) {
+    BigArgs &g = b->bg;
+    g.row_long = d + off[q++];
+    g.col_long = d + off[q++];
+    g.lr = d + off[q++];
+    g.lc = d + off[q++];
+    g.nlr = (int)lr.size();
+    g.nlc = (int)lc.size();
+    // LDS: scratch + queue slot + y [m]; the slice: the larger of the PDHG
+    // and polish layouts (and the scaling's vectors)
+    b->big_lds_bytes = sizeof(double) * ((size_t)MAX_WAVES * 10 + 2 + up2(b->m));
+    if (b->big_lds_bytes > 160 * 1024)
+      return fail(PH_EINVAL, "ph_batch_create: more than 20,000 rows; the big path keeps y in LDS");
+    g.ws_stride = std::max({big_pdhg_ws_len(b->n, b->m), big_pol_ws_len(b->n, b->m, y.nnzL, y.N),
+                            2 * up2(b->n) + up2(b->m)});
+    b->big = true;
+    b->mid_ready = false;
+    return PH_OK;
+  }
+  // LDS plan (doubles): see the carve at the top of solve_mid
   const int nw = b->mblock / WAVE;
   tr.nlong = (int)rln.size();
   tc.nlong = (int)cln.size();
@@ -3001,12 +3064,10 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
   // scaling-kernel geometry (lines per thread); the one-wave scenarios
   // (n + m <= POLISH_MAX) keep pdhg_kernel<64,1,E> with the active-set cache,
   // everything larger goes to the mid-size path (solve_mid)
-  if (!pick_geometry(n, m, 0, 0, &b->block, &b->per, &b->ext)) {
-    delete b;
-    return fail(PH_EINVAL, "ph_batch_create: scenario has more than 3072 rows or columns; the "
-                           "on-chip solver does not cover it");
-  }
-  const bool small = b->block == WAVE && b->per == 1 && n + m <= POLISH_MAX &&
+  // (scenarios with more than 3072 rows or columns have no register
+  // geometry: the big path, solve_big.inc)
+  const bool fits = pick_geometry(n, m, 0, 0, &b->block, &b->per, &b->ext);
+  const bool small = fits && b->block == WAVE && b->per == 1 && n + m <= POLISH_MAX &&
                      pick_geometry(n, m, b->xr, b->xc, &b->block, &b->per, &b->ext);
   int rc = 0;
   // (one-wave batches set it up too: their rescue polish for scenarios the
@@ -3108,15 +3169,30 @@ int ph_batch_bind(ph_batch_t b, const double *vals, const double *c, const doubl
     HIP_OK(hipMemcpyAsync(b->d_rl, rl, Sm * 8, hipMemcpyDeviceToDevice, b->stream));
     HIP_OK(hipMemcpyAsync(b->d_ru, ru, Sm * 8, hipMemcpyDeviceToDevice, b->stream));
   }
-  const size_t lds = scale_lds_bytes(b);
-  if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_batch_bind: scenario does not fit in LDS (nnz+2n+2m too large)");
   if (b->d_cache_ok) HIP_OK(hipMemsetAsync(b->d_cache_ok, 0, sizeof(int32_t) * b->S, b->stream));
   Pattern P{b->d_row_ptr, b->d_col_idx, b->d_col_ptr, b->d_csc_row, b->d_csc_k};
-  DISPATCH_GEOM(b->block, b->per, 0, {
-    hipLaunchKernelGGL((scale_kernel<B_, P_, P_>), dim3(b->S), dim3(B_), lds, b->stream,
-                       b->S, b->n, b->m, b->nnz, P, vals, b->d_vals_s, b->d_dr, b->d_dc, b->d_eta);
-  });
-  HIP_OK(hipGetLastError());
+  if (b->big) {
+    // the big path: the scaling with its working arrays in HBM (one block
+    // per scenario on the resident grid), then the CSC-ordered copy
+    if (int rc = big_init(b)) return rc;
+    hipLaunchKernelGGL(big_scale_kernel, dim3(b->big_grid), dim3(BIG_BLOCK), 0, b->stream, b->S, b->n,
+                       b->m, b->nnz, P, vals, b->d_vals_s, b->d_dr, b->d_dc, b->d_eta, b->bg);
+    HIP_OK(hipGetLastError());
+    const long tot = (long)b->S * b->nnz;
+    hipLaunchKernelGGL(big_transpose_kernel, dim3((int)std::min<long>((tot + 255) / 256, 65536)), dim3(256),
+                       0, b->stream, b->S, b->nnz, (const int32_t *)b->d_csc_k, (const double *)b->d_vals_s,
+                       b->d_vals_t);
+    HIP_OK(hipGetLastError());
+  } else {
+    const size_t lds = scale_lds_bytes(b);
+    if (lds > 160 * 1024)
+      return fail(PH_EINVAL, "ph_batch_bind: scenario does not fit in LDS (nnz+2n+2m too large)");
+    DISPATCH_GEOM(b->block, b->per, 0, {
+      hipLaunchKernelGGL((scale_kernel<B_, P_, P_>), dim3(b->S), dim3(B_), lds, b->stream,
+                         b->S, b->n, b->m, b->nnz, P, vals, b->d_vals_s, b->d_dr, b->d_dc, b->d_eta);
+    });
+    HIP_OK(hipGetLastError());
+  }
   if (polish_fits(b) || b->mid) {
     if (!b->d_sb) {
       int rc = dalloc(&b->d_sb, (size_t)b->S * (4 * b->n + 3 * b->m));
@@ -3201,6 +3277,12 @@ constexpr int PROF_SLOTS = 32;
 // small grid-strided grid.
 static int launch_bound(ph_batch *b, const SolveArgs &a, const int32_t *list, const int32_t *count) {
   if (!b->d_sb) return PH_OK;
+  if (b->big) {  // (every scenario; r and y in the workspace slices)
+    hipLaunchKernelGGL(big_bound_kernel, dim3(b->big_grid), dim3(BIG_BLOCK), BIG_SMALL_LDS, b->stream, a,
+                       b->bg);
+    HIP_OK(hipGetLastError());
+    return PH_OK;
+  }
   const size_t lds = sizeof(double) * (((size_t)b->n + 1 & ~(size_t)1) + ((size_t)b->m + 1 & ~(size_t)1) + MAX_WAVES);
   if (list)
     hipLaunchKernelGGL(bound_list_kernel<256>, dim3(std::min(b->S, TAIL_GRID)), dim3(256), lds,
@@ -3242,9 +3324,47 @@ static bool mid_full_grid() {
   return f;
 }
 
+// PHGPU_MID_GRID: cap of the resident grid of the mid-size / big phase
+// kernels (read per batch; the parity tests push several scenarios through
+// each block's work-queue loop and its workspace slice with a small grid).
+static int mid_grid_cap() {
+  const char *e = std::getenv("PHGPU_MID_GRID");
+  return e ? std::max(0, std::atoi(e)) : 0;
+}
+
+// First-use setup of the big path (at bind: the scaling runs on its
+// workspace): occupancy, the resident grid, the workspace slices, the
+// phase work lists.
+static int big_init(ph_batch *b) {
+  if (b->big_grid != 0) return PH_OK;
+  int per_cu = 0, per_cu_p = 0, cus = 0, dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  HIP_OK(hipFuncSetAttribute((const void *)big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)b->big_lds_bytes));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, big_kernel, BIG_BLOCK, b->big_lds_bytes));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, big_polish_kernel, BIG_BLOCK,
+                                                      BIG_SMALL_LDS));
+  if (per_cu < 1 || per_cu_p < 1) return fail(PH_EINVAL, "ph_batch_bind: the big-path kernels cannot be resident");
+  int grid = std::min(b->S, std::min(per_cu, per_cu_p) * std::max(1, cus));
+  if (const int cap = mid_grid_cap()) grid = std::min(grid, cap);
+  b->big_grid = grid;
+  b->bg.ws_blocks = grid;
+  int rc = 0;
+  if ((rc = dalloc(&b->d_bws, (size_t)grid * b->bg.ws_stride)) ||
+      (rc = dalloc(&b->d_vals_t, (size_t)b->S * b->nnz)) || (rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) ||
+      (rc = dalloc(&b->d_mctr, 16)))
+    return rc;
+  b->bg.ws_g = b->d_bws;
+  b->bg.vals_t = b->d_vals_t;
+  b->mid_grid = b->mid_pgrid = grid;
+  return PH_OK;
+}
+
 // First-use setup of the mid-size kernels: LDS limits, occupancy, the HBM
 // polish workspace (when it does not fit in LDS), the work lists.
 static int mid_init(ph_batch *b) {
+  if (b->big) return big_init(b);
   if (b->mid_grid != 0) return PH_OK;
   int per_cu = 0, per_cu_p = 0, cus = 0, dev = 0;
   HIP_OK(hipGetDevice(&dev));
@@ -3263,15 +3383,9 @@ static int mid_init(ph_batch *b) {
     return fail(PH_EINVAL, "ph_pdhg_solve: the mid-size kernels cannot be resident");
   b->mid_grid = std::min(b->S, per_cu * std::max(1, cus));
   b->mid_pgrid = std::min(b->S, per_cu_p * std::max(1, cus));
-  {  // PHGPU_MID_GRID: cap the resident grid (read per batch; the parity
-     // tests push several scenarios through each block's work-queue loop
-     // and its workspace slice with a small grid)
-    const char *e = std::getenv("PHGPU_MID_GRID");
-    const int cap = e ? std::atoi(e) : 0;
-    if (cap > 0) {
-      b->mid_grid = std::min(b->mid_grid, cap);
-      b->mid_pgrid = std::min(b->mid_pgrid, cap);
-    }
+  if (const int cap = mid_grid_cap()) {
+    b->mid_grid = std::min(b->mid_grid, cap);
+    b->mid_pgrid = std::min(b->mid_pgrid, cap);
   }
   // the HBM polish workspace: one slice per block of every launch that runs
   // the polish (mid_polish_kernel; on one-wave batches rescue_kernel and
@@ -3325,6 +3439,12 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
                   double exit_err, int first, int hand_at_limit) -> int {
     const MidPhase ph{in, cin, out, cout, q, exit_err, first, 0, hand_at_limit};
     if (int rc = phase_event(b, 0)) return rc;
+    if (b->big) {
+      hipLaunchKernelGGL(big_kernel, dim3(b->big_grid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream, a,
+                         b->bg, ph);
+      HIP_OK(hipGetLastError());
+      return phase_event(b, -1);
+    }
     DISPATCH_MID({
       hipLaunchKernelGGL((mid_kernel<B_, C_, R_>), dim3(mid_full_grid() ? b->S : b->mid_grid), dim3(B_),
                          b->mid_lds_bytes,
@@ -3337,6 +3457,12 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
                     int mode) -> int {
     const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode, 0, 0};
     if (int rc = phase_event(b, 1)) return rc;
+    if (b->big) {
+      hipLaunchKernelGGL(big_polish_kernel, dim3(b->big_grid), dim3(BIG_BLOCK), BIG_SMALL_LDS, b->stream,
+                         a, b->md, b->bg, ph);
+      HIP_OK(hipGetLastError());
+      return phase_event(b, -1);
+    }
     DISPATCH_MID({
       hipLaunchKernelGGL((mid_polish_kernel<B_, C_, R_>), dim3(mid_full_grid() ? b->S : b->mid_pgrid),
                          dim3(B_),
@@ -3904,7 +4030,8 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
-                  b->d_ctl, b->d_sym, b->d_ws, b->d_mlist, b->d_mctr, b->d_err,
+                  b->d_ctl, b->d_sym, b->d_ws, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
+                  b->d_bws,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

@@ -288,11 +288,18 @@ def _kkt_solve(c, q, Ad, rl, ru, l, u, atl, atu, rtl, rtu):
     return x, y
 
 
+# scenarios with more lines than this avoid the dense paths (lstsq on the
+# dense KKT matrix): farmer crops_multiplier 1000 has 21,001 lines
+DENSE_MAX = 2000
+
+
 def _pdas(x0, c, q, A, rl, ru, l, u, tau, kkt_tol, rounds=20):
     """Primal-dual active-set iterations from the active set of x0 (the same
     rule as the GPU polish): accepted when the clipped point passes the KKT
-    check.  Returns (err, x, y) of the best point."""
-    Ad = sp.csr_matrix(A).toarray()
+    check.  Returns (err, x, y) of the best point.  Large scenarios solve
+    each active set's KKT system by the regularised sparse LU (_kkt_reg)."""
+    large = A.shape[0] + A.shape[1] > DENSE_MAX
+    Ad = sp.csr_matrix(A) if large else sp.csr_matrix(A).toarray()
     ax = Ad @ x0
     eq = np.isfinite(l) & (l == u)
     atl = eq | (np.isfinite(l) & (np.abs(x0 - l) <= tau * (1 + np.abs(l))))
@@ -307,7 +314,13 @@ def _pdas(x0, c, q, A, rl, ru, l, u, tau, kkt_tol, rounds=20):
         if key in seen:
             break
         seen.add(key)
-        xu, y = _kkt_solve(c, q, Ad, rl, ru, l, u, atl, atu, rtl, rtu)
+        if large:
+            try:
+                xu, y = _kkt_reg(c, q, Ad, rl, ru, l, u, atl, atu, rtl, rtu)
+            except RuntimeError:  # singular factor
+                break
+        else:
+            xu, y = _kkt_solve(c, q, Ad, rl, ru, l, u, atl, atu, rtl, rtu)
         x = np.minimum(np.maximum(xu, l), u)
         pv, dv = kkt_residual(x, y, c, q, A, rl, ru, l, u)
         err = max(pv, dv)
@@ -374,7 +387,14 @@ def solve_scenario(c, q, A, rl, ru, l, u, kkt_tol=1e-9):
                 best = bp
             if bp[0] <= kkt_tol:
                 return bp[1], bp[2], True
+    large = A.shape[0] + A.shape[1] > DENSE_MAX
+    if not np.any(q) and large:
+        # a large LP's simplex vertex is exact to its tolerances (the dense
+        # polish below is for small degenerate QP/LP cases)
+        return x, rowdual, True
     for tau in (1e-7, 1e-8, 1e-6, 1e-9, 1e-5, 1e-10, 1e-4):
+        if large:
+            break
         xp, yp = _polish(x, c, q, A, rl, ru, l, u, tau)
         pv, dv = kkt_residual(xp, yp, c, q, A, rl, ru, l, u)
         err = max(pv, dv)

@@ -704,3 +704,73 @@ def test_variable_probability_w_mask_matches_oracle(device_loop):
     assert abs(conv - oc) <= 1e-3 * abs(oc)
     assert abs(eobj - oe) <= 1e-5 * abs(oe)
     assert abs(tb - ot) <= 1e-6 * abs(ot)
+
+
+def test_farmer_c1000_big_path_matches_oracle(monkeypatch):
+    """SURVEY.md 8(d) F4's scenario shape (farmer crops_multiplier 1000:
+    12,000 columns, 9,001 rows, 27,000 nonzeros, a 3,000-entry row) through
+    the big path (csrc/solve_big.inc: state in HBM workspace slices, the
+    streaming PDHG, the LDL' polish over the slice), 3 scenarios from scen3
+    on a 2-block resident grid (the work queue).  Iter0 (LPs): the trivial
+    bound to 1e-7 and the nonants (unique optimum) to 1e-6 against the
+    oracle's simplex.  Three PH iterations (host loop): Compute_Xbar /
+    Update_W against the oracle's restatement on the same x, and every
+    prox-QP solve certified by the oracle's KKT check of the oracle's own QP
+    data (a KKT point of a convex QP is its optimum; HiGHS' QP at this size
+    needs minutes per solve).  Then the device loop (graph replay) from the
+    same start reproduces the host loop."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    from oracle.solve import kkt_residual
+    monkeypatch.setenv("PHGPU_MID_GRID", "2")
+    names = [f"scen{i}" for i in range(3, 6)]
+    c = 1000
+
+    def run(device_loop):
+        opts = _opts(PHIterLimit=3, defaultPHrho=1.0, convthresh=-1.0, device_loop=device_loop)
+        ph = PH(dict(opts), names, farmer.scenario_creator,
+                scenario_creator_kwargs={"crops_multiplier": c})
+        ph.PH_Prep()
+        ph.subproblem_creation()
+        return ph, opts
+
+    ph, opts = run(False)
+    tb = ph.Iter0()
+    b = ph.batch
+    assert (b.n, b.m, b.nnz) == (12000, 9001, 27000)
+    assert np.all(b.status.cpu().numpy() == 0)
+    orc = OraclePH(dict(opts), [om.farmer(nm, c) for nm in names])
+    ot = orc.Iter0()
+    assert abs(tb - ot) <= 1e-7 * abs(ot), (tb, ot)
+    S, n, m = b.S, b.n, b.m
+    cols = ph.batch_data.nonant_cols
+    X = b.x.view(n, S).cpu().numpy()
+    xo = np.array([orc.x[s][orc.scens[s].nonant_idx] for s in range(S)]).T
+    assert _rel(X[cols], xo) < 1e-6
+    for k in range(1, 4):
+        ph.Compute_Xbar()
+        ph.Update_W(False)
+        X = b.x.view(n, S).cpu().numpy()
+        orc.x = [X[:, s].copy() for s in range(S)]
+        orc.Compute_Xbar()
+        orc.Update_W()
+        assert _rel(ph.xbar.view(ph.K, S).cpu().numpy().T, np.array(orc.xbar)) < 1e-12
+        assert _rel(ph.W.view(ph.K, S).cpu().numpy().T, np.array(orc.W)) < 1e-12
+        ph.solve_loop(solver_options=ph.current_solver_options)
+        assert np.all(b.status.cpu().numpy() == 0), k
+        X = b.x.view(n, S).cpu().numpy()
+        Y = b.y.view(m, S).cpu().numpy()
+        for s in range(S):
+            sc = orc.scens[s]
+            g, q, _ = orc._terms(s, 1.0, 1.0)
+            pv, dv = kkt_residual(X[:, s], Y[:, s], g, q, sc.A, sc.rl, sc.ru, sc.l, sc.u)
+            assert max(pv, dv) < 1e-7, (k, s, pv, dv)
+    eobj_host = ph.Eobjective()
+    W_host = ph.W.cpu().numpy().copy()
+    # the device loop (graph replay of the big kernels) from a fresh Iter0
+    ph2, _ = run(True)
+    ph2.Iter0()
+    ph2.iterk_loop()
+    assert ph2._PHIter == 3
+    assert _rel(ph2.W.cpu().numpy(), W_host) < 1e-7
+    assert abs(ph2.Eobjective() - eobj_host) <= 1e-9 * abs(eobj_host)
