@@ -146,11 +146,11 @@ def cpu_baseline(c, scens, convthresh, cores=16, f3_crops=100, f3_sample=64, f3_
 
 def workload_tag(kind, S_loc, c=None):
     """The workload tag tools/pmc_summary.py writes into a PMC summary
-    (farmer10k_c1, farmer10k_c100, sslp10k), or None for a size no
-    committed profile describes."""
-    if S_loc != 10000:
+    (farmer10k_c1, farmer10k_c100, farmer1k_c1000, sslp10k), or None for a
+    size no committed profile describes."""
+    if S_loc % 1000 or S_loc == 0:
         return None
-    return f"farmer10k_c{c}" if kind == "farmer" else "sslp10k"
+    return f"farmer{S_loc // 1000}k_c{c}" if kind == "farmer" else f"sslp{S_loc // 1000}k"
 
 
 def pmc_traffic(kname, tag):
@@ -292,6 +292,78 @@ def hbm_config(args, world, farmer, PH, opts):
                                              "from HBM would need -- a work rate, not a measurement"}}
 
 
+def big_config(args, world, farmer, PH, opts):
+    """farmer crops_multiplier --f4-crops (1000: n=12,000,
+    m=9,001, nnz=27,000 per scenario), --f4-scens scenarios per rank (1000,
+    the published EF's size), through the big path (csrc/solve_big.inc: the
+    streaming PDHG with its state in HBM, the LDL' polish).  Iter0, one PH
+    iteration of warmup, then --hbm-steps timed PH iterations (eager device
+    loop) with the library's per-launch HIP events.
+
+    roofline: the big_kernel (PDHG phase) as the dominant streaming kernel:
+    algorithmic bytes = SURVEY 8(d) B_it = 8 (2 nnz + 7 n + 5 m) per
+    scenario-step x the PDHG steps its launches took, over its launch time;
+    `traffic` = the PMC-measured bytes of the same launches when a profile
+    of this workload is committed.  The trivial bound is a lower bound of the
+    published EF (-1.334838651e8 at S=1000, c=1000,
+    paperruns/scripts/farmer/ef_1000_1000.out:183)."""
+    c = args.f4_crops
+    S = args.f4_scens * world
+    o = dict(opts)
+    ph = PH(o, [f"scen{i}" for i in range(S)], farmer.scenario_creator,
+            scenario_creator_kwargs={"crops_multiplier": c})
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    ph._create_solvers()
+    b = ph.batch
+    torch.cuda.synchronize()
+    _progress("F4 Iter0")
+    t0 = time.perf_counter()
+    tb = ph.Iter0()
+    torch.cuda.synchronize()
+    t_iter0 = time.perf_counter() - t0
+    nonopt0 = b.summary()[0]
+    ph.PHoptions["device_loop_graphs"] = False
+    ph.run_device_loop(0, 1, -1.0, chunk=1)
+    b.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ph.run_device_loop(1, 1 + args.hbm_steps, -1.0, chunk=args.hbm_steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n_t, _, _, _, nk, k_ms, np_, p_ms = b.read_timing_full()
+    st = b.loop_status()
+    b.set_timing(False)
+    d = torch.tensor([dt], dtype=torch.float64, device=_red_dev())
+    if world > 1:
+        dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    dt = float(d.item())
+    n, m, nnz = b.n, b.m, b.nnz
+    bit = 8 * (2 * nnz + 7 * n + 5 * m)
+    steps = st[4]
+    gbs = steps * bit / (k_ms / 1000.0) / 1e9 if k_ms > 0 else 0.0
+    trf = pmc_traffic("big_kernel", workload_tag("farmer", ph.S_loc, c))[0]
+    return {"workload": f"farmer PH, {S} scenarios ({args.f4_scens} per GPU), crops_multiplier={c} "
+                        f"(n={n}, m={m}, nnz={nnz} per scenario), rho={args.rho}",
+            "value": round(S * args.hbm_steps / dt, 2), "unit": "solves/s",
+            "ms_per_step": round(dt / args.hbm_steps * 1000.0, 3), "steps": args.hbm_steps,
+            "iter0_s": round(t_iter0, 3), "iter0_not_optimal": nonopt0, "trivial_bound": tb,
+            "published_ef": -1.334838651e8 if (S == 1000 and c == 1000) else None,
+            "pdhg_steps_per_solve": round(steps / max(st[3], 1), 1), "pdhg_steps_max": st[5],
+            "polished_per_solve": round(st[6] / max(st[3], 1), 3), "not_optimal_in_window": st[2],
+            "roofline": {"bound": "hbm", "kernel": "big_kernel (streaming PDHG phase)",
+                         "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "traffic": None if trf is None or not nk else round(trf),
+                         "alg_bytes_per_scenario_step": bit, "pdhg_steps": steps,
+                         "kernel_ms": round(k_ms, 3), "launches": nk,
+                         "polish_ms": round(p_ms, 3), "polish_launches": np_,
+                         "note": "achieved = SURVEY 8(d) B_it x PDHG steps of the window / the "
+                                 "big_kernel launches' HIP-event time"}}
+
+
 def sslp_config(args, world, PH, opts):
     """BASELINE config 5: sslp_15_45 LP relaxation (n=705, m=60, nnz=1364 per
     scenario; synthetic scenarios, ClientPresent ~ Bernoulli(0.5) seeded per
@@ -427,6 +499,9 @@ def _parser():
     ap.add_argument("--graphs", type=int, default=1,
                     help="replay the timed device-loop chunk as a HIP graph (0: eager launches, "
                          "one ph_loop_pass call per PH iteration)")
+    ap.add_argument("--f4-scens", type=int, default=1000,
+                    help="scenarios per rank of the F4 companion config (big path); 0 = skip")
+    ap.add_argument("--f4-crops", type=int, default=1000)
     ap.add_argument("--sslp-scens", type=int, default=10000,
                     help="scenarios per rank of the sslp companion config (BASELINE config 5); 0 = skip")
     return ap
@@ -614,6 +689,11 @@ def run():
         f3 = hbm_config(args, world, farmer, PH, opts)
 
 
+    f4 = None
+    if args.f4_scens > 0:
+        _progress("companion config F4")
+        f4 = big_config(args, world, farmer, PH, opts)
+
     sslp = None
     if args.sslp_scens > 0:
         _progress("companion config sslp")
@@ -666,6 +746,7 @@ def run():
             "ph_to_tol_sample": tol_small,
             "cpu_baseline": cpu,
             "hbm_config": f3,
+            "f4_config": f4,
             "sslp_config": sslp,
         }
     else:

@@ -2558,7 +2558,12 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
 // (wc_s = 1 / (count of the reference rank holding s) / ref_n_proc, i.e.
 // phbase.py:254-276's per-rank means summed over ranks), into conv_hist, and
 // the stop test before the solve; the last block also clears the solve's
-// work-list counters.
+// work-list counters.  KL lanes per scenario (the block is POST_BLOCK/KL
+// consecutive scenarios x KL nonant lanes, scenario-fastest so each nonant
+// row's loads coalesce): with many nonants (farmer c=100: K = 300; c=1000:
+// 3,000 on 1,000 scenarios) one thread per scenario would leave a few
+// hundred waves walking K serially.
+template <int KL>
 __global__ void __launch_bounds__(POST_BLOCK) update_w_conv_kernel(
     int S, int K, const double *__restrict__ x, const int32_t *__restrict__ nonant_col,
     const double *__restrict__ sums, int G, const int32_t *__restrict__ gid,
@@ -2569,10 +2574,12 @@ __global__ void __launch_bounds__(POST_BLOCK) update_w_conv_kernel(
     double *__restrict__ part_out) {
   __shared__ double red[MAX_WAVES];
   if (stopped(ctl)) return;
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int SB = POST_BLOCK / KL;  // scenarios per block
+  const int sl = threadIdx.x % SB, kl = threadIdx.x / SB;
+  const int s = blockIdx.x * SB + sl;
   double acc = 0.0;
   if (s < S) {
-    for (int k = 0; k < K; ++k) {
+    for (int k = kl; k < K; k += KL) {
       const size_t o = (size_t)k * S + s;
       const int g = gid[o];
       const double xb = sums[g], xsq = sums[G + g];
@@ -2585,9 +2592,19 @@ __global__ void __launch_bounds__(POST_BLOCK) update_w_conv_kernel(
       W[o] = w;
       acc += fabs(d);
     }
-    absdiff[s] = acc;
   }
-  double v[1] = {s < S ? acc * wconv[s] : 0.0};
+  if constexpr (KL > 1) {  // the scenario's lanes summed in lane order (deterministic)
+    __shared__ double la[POST_BLOCK];
+    la[threadIdx.x] = acc;
+    __syncthreads();
+    if (kl == 0) {
+      double t = 0.0;
+      for (int q = 0; q < KL; ++q) t += la[q * SB + sl];
+      acc = t;
+    }
+  }
+  if (kl == 0 && s < S) absdiff[s] = acc;
+  double v[1] = {(kl == 0 && s < S) ? acc * wconv[s] : 0.0};
   block_sum<1>(v, red);
   if (threadIdx.x == 0) pub(part + blockIdx.x, v[0]);
   if (!last_block(ticket)) return;
@@ -3095,7 +3112,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
     ph_batch_destroy(b);
     return rc;
   }
-  b->part_cap = (size_t)((S + POST_BLOCK - 1) / POST_BLOCK);
+  b->part_cap = (size_t)((S + 7) / 8);  // (update_w_conv_kernel<32>: 8 scenarios per block)
   if (dalloc(&b->d_part, b->part_cap)) {
     ph_batch_destroy(b);
     return fail(PH_EHIP, "ph_batch_create: allocation failed");
@@ -3857,6 +3874,28 @@ int ph_loop_backup_status(ph_batch_t b, const int32_t *status, int32_t *status_s
   return PH_OK;
 }
 
+// update_w_conv_kernel with KL nonant lanes per scenario by the nonant count.
+static int launch_update_w_conv(ph_batch *b, const double *x, const double *sums, int32_t G,
+                                const int32_t *gid, const double *rho, const double *w_coeff,
+                                double *xbar, double *xsqbar, double *W, double *absdiff,
+                                const double *wconv, double *conv_hist, double *part_out) {
+  const int KL = b->K > 64 ? 32 : (b->K > 8 ? 8 : 1);
+  const int SB = POST_BLOCK / KL;
+  const int nb = (b->S + SB - 1) / SB;
+  if ((size_t)nb > b->part_cap) return fail(PH_EINVAL, "update_w_conv: reduction buffer too small");
+  auto go = [&](auto kl_c) {
+    constexpr int KLc = decltype(kl_c)::value;
+    hipLaunchKernelGGL(update_w_conv_kernel<KLc>, dim3(nb), dim3(POST_BLOCK), 0, b->stream, b->S, b->K,
+                       x, b->d_nonant_col, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
+                       b->d_part, b->d_ctr + 4, b->d_ctl, conv_hist, b->d_ctr, part_out);
+  };
+  if (KL == 32) go(std::integral_constant<int, 32>{});
+  else if (KL == 8) go(std::integral_constant<int, 8>{});
+  else go(std::integral_constant<int, 1>{});
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
 int ph_loop_update_w_conv(ph_batch_t b, const double *x, const double *sums, int32_t G,
                           const int32_t *gid, const double *rho, const double *w_coeff,
                           double *xbar, double *xsqbar, double *W, double *absdiff,
@@ -3865,14 +3904,8 @@ int ph_loop_update_w_conv(ph_batch_t b, const double *x, const double *sums, int
       !absdiff || !wconv || !conv_hist)
     return fail(PH_EINVAL, "ph_loop_update_w_conv: bad arguments (or loop not enabled)");
   if (!b->d_nonant_col || b->K == 0) return fail(PH_EINVAL, "ph_loop_update_w_conv: no nonants declared");
-  const int nb = (b->S + POST_BLOCK - 1) / POST_BLOCK;
-  if ((size_t)nb > b->part_cap)
-    return fail(PH_EINVAL, "ph_loop_update_w_conv: reduction buffer too small");
-  hipLaunchKernelGGL(update_w_conv_kernel, dim3(nb), dim3(POST_BLOCK), 0, b->stream, b->S, b->K, x,
-                     b->d_nonant_col, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
-                     b->d_part, b->d_ctr + 4, b->d_ctl, conv_hist, b->d_ctr, (double *)nullptr);
-  HIP_OK(hipGetLastError());
-  return PH_OK;
+  return launch_update_w_conv(b, x, sums, G, gid, rho, w_coeff, xbar, xsqbar, W, absdiff, wconv,
+                              conv_hist, nullptr);
 }
 
 int ph_loop_conv_local(ph_batch_t b, const double *absdiff, const int32_t *seg, int32_t R,
@@ -3909,8 +3942,6 @@ int ph_loop_pass(ph_batch_t b) {
   if (!b || !b->loop_on || !b->pass_bound)
     return fail(PH_EINVAL, "ph_loop_pass: loop not enabled or no pass bound");
   const ph_loop_pass_args &p = b->pass;
-  const int nb = (b->S + POST_BLOCK - 1) / POST_BLOCK;
-  if ((size_t)nb > b->part_cap) return fail(PH_EINVAL, "ph_loop_pass: reduction buffer too small");
   if (p.conv_part) {
     // several ranks: the previous pass's convergence test on its allreduced
     // partial (one pass late), then this pass's partial into the same slot
@@ -3919,11 +3950,9 @@ int ph_loop_pass(ph_batch_t b) {
                        b->d_ctr);
     HIP_OK(hipGetLastError());
   }
-  hipLaunchKernelGGL(update_w_conv_kernel, dim3(nb), dim3(POST_BLOCK), 0, b->stream, b->S, b->K,
-                     (const double *)p.x, b->d_nonant_col, p.sums, p.G, p.gid, p.rho, p.w_coeff,
-                     p.xbar, p.xsqbar, p.W, p.absdiff, p.wconv, b->d_part, b->d_ctr + 4, b->d_ctl,
-                     p.conv_hist, b->d_ctr, p.conv_part);
-  HIP_OK(hipGetLastError());
+  if (int rc = launch_update_w_conv(b, p.x, p.sums, p.G, p.gid, p.rho, p.w_coeff, p.xbar, p.xsqbar,
+                                    p.W, p.absdiff, p.wconv, p.conv_hist, p.conv_part))
+    return rc;
   if (p.conv_part) {
     const long nx = (long)b->n * b->S, ny = b->m ? (long)b->m * b->S : 0;
     const long mx = std::max(std::max(nx, ny), (long)b->S);
