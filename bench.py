@@ -496,7 +496,7 @@ def _parser():
     ap.add_argument("--hbm-crops", type=int, default=100,
                     help="crops_multiplier of the HBM-bound companion config (F3); 0 = skip")
     ap.add_argument("--hbm-steps", type=int, default=5)
-    ap.add_argument("--graphs", type=int, default=1,
+    ap.add_argument("--graphs", type=int, default=0,
                     help="replay the timed device-loop chunk as a HIP graph (0: eager launches, "
                          "one ph_loop_pass call per PH iteration)")
     ap.add_argument("--f4-scens", type=int, default=1000,

@@ -2802,17 +2802,21 @@ void build_chunks(int lines, const std::vector<int32_t> &ptr, std::vector<int32_
 // and PR rows per thread (instances listed in DISPATCH_MID).
 bool pick_mid(int n, int m, int *blk, int *pc, int *pr) {
   const int mx = n > m ? n : m;
-  {  // PHGPU_MID_GEOM=512: 512-thread blocks with up to 3 lines per thread
-     // (measurement hook: 1024-thread blocks are capped at 128 VGPRs and spill)
+  {  // 512-thread blocks with up to 3 columns and 3 rows per thread while
+     // max(n, m) <= 1536: 256 VGPRs per thread instead of the 1024-thread
+     // blocks' 128 (whose polish spilled 172 VGPRs at F3).  Measured at F3
+     // iterations 30-34 (tools/mid_polish_prof.py): 14.3 ms per PH iteration
+     // against 16.0 with <1024,2,1> (profiles/r03/mid_polish_f3_geom512.txt).
+     // PHGPU_MID_GEOM=1024 keeps the 1024-thread instances (measurement hook).
     static const int g = [] {
       const char *e = std::getenv("PHGPU_MID_GEOM");
-      return e ? std::atoi(e) : 0;
+      return e ? std::atoi(e) : 512;
     }();
     if (g == 512 && mx > 512 && n <= 1536 && m <= 1536) {
       *blk = 512;
       *pc = (n + 511) / 512;
       *pr = (m + 511) / 512;
-      if (*pc == 3 && *pr == 2) return true;
+      return true;
     }
   }
   for (int B : {64, 128, 256, 512})
@@ -2844,6 +2848,10 @@ bool pick_mid(int n, int m, int *blk, int *pc, int *pr) {
     MID_CASE(1024, 3, 1, __VA_ARGS__) MID_CASE(1024, 3, 2, __VA_ARGS__)            \
     MID_CASE(1024, 1, 3, __VA_ARGS__) MID_CASE(1024, 2, 3, __VA_ARGS__)            \
     MID_CASE(1024, 3, 3, __VA_ARGS__) MID_CASE(512, 3, 2, __VA_ARGS__)             \
+    MID_CASE(512, 2, 1, __VA_ARGS__) MID_CASE(512, 1, 2, __VA_ARGS__)              \
+    MID_CASE(512, 2, 2, __VA_ARGS__) MID_CASE(512, 3, 1, __VA_ARGS__)              \
+    MID_CASE(512, 1, 3, __VA_ARGS__) MID_CASE(512, 2, 3, __VA_ARGS__)              \
+    MID_CASE(512, 3, 3, __VA_ARGS__)                                               \
     else return fail(PH_EINVAL, "internal: no mid-size kernel instance");          \
   } while (0)
 

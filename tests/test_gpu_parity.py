@@ -514,7 +514,7 @@ def test_farmer_c100_mid_path_matches_oracle(iters, grid, monkeypatch):
     if grid:
         monkeypatch.setenv("PHGPU_MID_GRID", str(grid))
     names = [f"scen{i}" for i in range(3, 15)]
-    opts = _opts(PHIterLimit=iters, defaultPHrho=1.0, convthresh=1e-7)
+    opts = _opts(PHIterLimit=iters, defaultPHrho=1.0, convthresh=1e-7, device_loop_graphs=True)
     ph = PH(dict(opts), names, farmer.scenario_creator,
             scenario_creator_kwargs={"crops_multiplier": 100})
     conv, eobj, tb = ph.ph_main()
@@ -727,7 +727,8 @@ def test_farmer_c1000_big_path_matches_oracle(monkeypatch):
     c = 1000
 
     def run(device_loop):
-        opts = _opts(PHIterLimit=3, defaultPHrho=1.0, convthresh=-1.0, device_loop=device_loop)
+        opts = _opts(PHIterLimit=3, defaultPHrho=1.0, convthresh=-1.0, device_loop=device_loop,
+                     device_loop_graphs=True)
         ph = PH(dict(opts), names, farmer.scenario_creator,
                 scenario_creator_kwargs={"crops_multiplier": c})
         ph.PH_Prep()
