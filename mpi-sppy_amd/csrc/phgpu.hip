@@ -2945,7 +2945,9 @@ static int big_init(ph_batch *b);
 // state in HBM workspace slices.
 static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx,
                      const std::vector<int32_t> &col_ptr) {
-  const bool big = !pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr);
+  // PHGPU_FORCE_BIG=1: measurement hook, the big path for a mid-size shape
+  const char *fb = std::getenv("PHGPU_FORCE_BIG");
+  const bool big = (fb && std::atoi(fb) != 0) || !pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr);
   if (big) {
     b->mblock = BIG_BLOCK;
     b->mpc = b->mpr = 0;

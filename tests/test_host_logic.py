@@ -360,3 +360,55 @@ def test_variable_probability_matches_oracle():
     with pytest.raises(RuntimeError, match="do not sum to 1"):
         PH(dict(opts), names, farmer.scenario_creator,
            variable_probability=lambda sc, first_name=None: [(first_name, 0.5)])
+
+
+def _farmer3_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "mpi-sppy_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mpisppy_amd.examples import doc_farmer
+        names = ["good", "average", "bad"]
+        opts = _opts(PHIterLimit=5, defaultPHrho=10, convthresh=1e-7)
+        ph, conv, eobj, tb = _run_ph(opts, names, doc_farmer.scenario_creator)
+        v = ph.gather_var_values_to_rank0()
+        q.put((rank, conv, eobj, tb, ph._PHIter, list(ph.local_scenario_names), v))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_three_rank_gloo_doc_farmer_config1():
+    """BASELINE config 1 ("farmer 3-scenario PH on CPU via mpiexec -n 3",
+    examples/run_all.py:80-83): the doc farmer on three gloo ranks, one
+    scenario per rank (sputils.py:625-628), through the host flow with the
+    CPU stand-in batch (the product solver needs the GPU): the published
+    per-scenario nonants after 5 PH iterations (doc/src/examples.rst:323-334)
+    and the oracle's conv / Eobj / trivial bound on 3 reference ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_farmer3_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[5] for r in res] == [["good"], ["average"], ["bad"]]
+    opts = _opts(PHIterLimit=5, defaultPHrho=10, convthresh=1e-7)
+    orc = OraclePH(opts, [om.doc_farmer(n) for n in ("good", "average", "bad")], n_proc=3)
+    oc, oe, ot = orc.ph_main()
+    for rank, conv, eobj, tb, iters, _, _ in res:
+        assert iters == orc.iters == 5
+        assert abs(conv - oc) < 1e-8 * abs(oc)
+        assert abs(eobj - oe) < 1e-8 * abs(oe)
+        assert abs(tb - ot) < 1e-8 * abs(ot)
+    v = res[0][6]
+    ref = {("good", "X[BEETS]"): 280.6489711937925, ("average", "X[WHEAT]"): 136.72037037055298,
+           ("bad", "X[CORN]"): 85.26131687116226}
+    for k, r in ref.items():
+        assert abs(v[k] - r) / abs(r) < 1e-8, (k, v[k], r)
