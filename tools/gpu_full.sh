@@ -1,13 +1,17 @@
 #!/bin/bash
 # One GPU call: rocprofv3 kernel stats + PMC HBM passes of each bench
-# workload ON ITS OWN (F2 headline, F3 c=100, sslp), the per-kernel traffic
+# workload ON ITS OWN (F2 headline, F3 c=100, sslp, F4 c=1000), the per-kernel traffic
 # summaries (tools/pmc_summary.py refuses a window of another workload's
 # kernels), then the default bench line.
-# Usage: bash tools/gpu_full.sh [round-tag]   (outputs under gpurun_out/)
+# Usage: bash tools/gpu_full.sh [round-tag] ["f2 f3 sslp f4" | ... ] [bench]
+#   (outputs under gpurun_out/; the default profiles all four, then benches)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out
 TAG=${1:-r03}
+SEL=${2:-"f2 f3 sslp f4"}
+BENCH=${3:-bench}
+on() { [[ " $SEL " == *" $1 "* ]]; }
 mkdir -p $O $R/profiles/$TAG
 cd $R
 export TMPDIR=/tmp
@@ -20,10 +24,12 @@ prof() {  # name, window, workload tag, bench args...
   cp $O/pmc_summary_$N.json profiles/$TAG/pmc_summary_$N.json
   cp $O/${N}_stats/run_kernel_stats.csv profiles/$TAG/${N}_kernel_stats.csv 2>/dev/null || cp $(find $O/${N}_stats -name '*kernel_stats.csv' | head -1) profiles/$TAG/${N}_kernel_stats.csv
 }
-ONE="--tol-run 0 --no-cpu-baseline --hbm-crops 0 --sslp-scens 0"
-prof f2 20 farmer10k_c1 $ONE || exit 1
-prof f3 5 farmer10k_c100 $ONE --crops 100 --steps 5 --warmup 5 || exit 1
-prof sslp 5 sslp10k --tol-run 0 --no-cpu-baseline --hbm-crops 0 --scens 1000 --steps 5 --warmup 5 --sslp-scens 10000 || exit 1
+ONE="--tol-run 0 --no-cpu-baseline --hbm-crops 0 --sslp-scens 0 --f4-scens 0"
+on f2 && { prof f2 20 farmer10k_c1 $ONE || exit 1; }
+on f3 && { prof f3 5 farmer10k_c100 $ONE --crops 100 --steps 5 --warmup 5 || exit 1; }
+on sslp && { prof sslp 5 sslp10k --tol-run 0 --no-cpu-baseline --hbm-crops 0 --f4-scens 0 --scens 1000 --steps 5 --warmup 5 --sslp-scens 10000 || exit 1; }
+on f4 && { prof f4 3 farmer1k_c1000 --tol-run 0 --no-cpu-baseline --hbm-crops 0 --sslp-scens 0 --scens 1000 --steps 5 --warmup 5 --f4-scens 1000 --hbm-steps 3 || exit 1; }
+[ "$BENCH" = bench ] || { echo ALLDONE; exit 0; }
 timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json
 cp $O/bench.json profiles/$TAG/bench_farmer10k_c1.json

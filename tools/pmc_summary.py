@@ -16,11 +16,12 @@ to it (a window that caught another config's launches is what mislabelled
 the round-2 profiles):
 
   farmer10k_c1    active_set_kernel exactly once per solve, no mid-size kernel
-  farmer10k_c100  mid_kernel<1024, 2, 1> / mid_polish_kernel<1024, 2, 1> only
-                  (n = 1200, m = 901), no active_set_kernel
+  farmer10k_c100  mid_kernel<512, 3, 2> / mid_polish_kernel<512, 3, 2> only
+                  (n = 1200, m = 901; 512-thread instances since round 3),
+                  no active_set_kernel
   farmer1k_c1000  big_kernel / big_polish_kernel (the big path: n = 12,000,
                   m = 9,001), no one-wave or mid-size kernel
-  sslp10k         mid_kernel<1024, 1, 1> / mid_polish_kernel<1024, 1, 1> only
+  sslp10k         mid_kernel<512, 2, 1> / mid_polish_kernel<512, 2, 1> only
                   (n = 705, m = 60)
 
 Window: the launches after the (WINDOW+1)-th last `summary_kernel` dispatch,
@@ -47,15 +48,15 @@ WORKLOADS = {
                      "require": {"active_set_kernel": None}, "forbid": ["mid_kernel", "mid_polish_kernel"],
                      "once_per_solve": ["active_set_kernel"]},
     "farmer10k_c100": {"scenarios_per_rank": 10000, "crops_multiplier": 100,
-                       "require": {"mid_kernel": "mid_kernel<1024, 2, 1>",
-                                   "mid_polish_kernel": "mid_polish_kernel<1024, 2, 1>"},
+                       "require": {"mid_kernel": "mid_kernel<512, 3, 2>",
+                                   "mid_polish_kernel": "mid_polish_kernel<512, 3, 2>"},
                        "forbid": ["active_set_kernel"], "once_per_solve": []},
     "farmer1k_c1000": {"scenarios_per_rank": 1000, "crops_multiplier": 1000,
                        "require": {"big_kernel": "big_kernel", "big_polish_kernel": "big_polish_kernel"},
                        "forbid": ["active_set_kernel", "mid_kernel"], "once_per_solve": []},
     "sslp10k": {"scenarios_per_rank": 10000, "crops_multiplier": None,
-                "require": {"mid_kernel": "mid_kernel<1024, 1, 1>",
-                            "mid_polish_kernel": "mid_polish_kernel<1024, 1, 1>"},
+                "require": {"mid_kernel": "mid_kernel<512, 2, 1>",
+                            "mid_polish_kernel": "mid_polish_kernel<512, 2, 1>"},
                 "forbid": ["active_set_kernel"], "once_per_solve": []},
 }
 
