@@ -100,33 +100,55 @@ struct KktSymbolic {
       error = "the minimum-degree order did not cover every vertex";
       return false;
     }
-    pos.assign(N, 0);
-    for (int c = 0; c < N; ++c) pos[order[c]] = c;
-    // ---- symbolic factorisation: pattern(c) = {pos[a] > c} U children's patterns
-    std::vector<std::vector<int32_t>> pat(N);
-    std::vector<int32_t> parent(N, -1);
-    std::vector<std::vector<int32_t>> kids(N);
-    std::fill(mark.begin(), mark.end(), -1);
-    for (int c = 0; c < N; ++c) {
-      auto &P = pat[c];
-      const int v = order[c];
-      for (int a : adj[v])
-        if (pos[a] > c && mark[pos[a]] != c) {
-          P.push_back(pos[a]);
-          mark[pos[a]] = c;
-        }
-      for (int k : kids[c])
-        for (int r : pat[k])
-          if (r > c && mark[r] != c) {
-            P.push_back(r);
-            mark[r] = c;
+    // ---- symbolic factorisation: pattern(c) = {pos[a] > c} U children's
+    // patterns; then once more in level order (leaves first, the columns
+    // of a level contiguous): a topological order of the elimination tree
+    // has the same fill, and the device then finds level l's columns at
+    // lvp[l] .. lvp[l+1] and their CSC entries at Lcp[lvp[l]] .. without an
+    // indirection (lvc and lee are the identity).
+    std::vector<std::vector<int32_t>> pat;
+    std::vector<int32_t> parent, level;
+    auto symbolic = [&]() {
+      pos.assign(N, 0);
+      for (int c = 0; c < N; ++c) pos[order[c]] = c;
+      pat.assign(N, {});
+      parent.assign(N, -1);
+      std::vector<std::vector<int32_t>> kids(N);
+      std::fill(mark.begin(), mark.end(), -1);
+      for (int c = 0; c < N; ++c) {
+        auto &P = pat[c];
+        const int v = order[c];
+        for (int a : adj[v])
+          if (pos[a] > c && mark[pos[a]] != c) {
+            P.push_back(pos[a]);
+            mark[pos[a]] = c;
           }
-      std::sort(P.begin(), P.end());
-      if (!P.empty()) {
-        parent[c] = P[0];
-        kids[P[0]].push_back(c);
+        for (int k : kids[c])
+          for (int r : pat[k])
+            if (r > c && mark[r] != c) {
+              P.push_back(r);
+              mark[r] = c;
+            }
+        std::sort(P.begin(), P.end());
+        if (!P.empty()) {
+          parent[c] = P[0];
+          kids[P[0]].push_back(c);
+        }
       }
+      level.assign(N, 0);  // levels of the elimination tree (leaves 0)
+      for (int c = 0; c < N; ++c)
+        if (parent[c] >= 0) level[parent[c]] = std::max(level[parent[c]], level[c] + 1);
+    };
+    symbolic();
+    {
+      std::vector<int32_t> byl(N);
+      for (int c = 0; c < N; ++c) byl[c] = c;
+      std::stable_sort(byl.begin(), byl.end(), [&](int a, int b) { return level[a] < level[b]; });
+      std::vector<int32_t> o2(N);
+      for (int c = 0; c < N; ++c) o2[c] = order[byl[c]];
+      order.swap(o2);
     }
+    symbolic();
     {  // sizes in 64 bits first: a dense trailing block of a few thousand
        // vertices overflows int32 in the update lists
       long long nl = 0, nc = 0;
@@ -167,10 +189,7 @@ struct KktSymbolic {
           Lrq[q] = p;
         }
     }
-    // ---- levels of the elimination tree (leaves 0)
-    std::vector<int32_t> level(N, 0);
-    for (int c = 0; c < N; ++c)
-      if (parent[c] >= 0) level[parent[c]] = std::max(level[parent[c]], level[c] + 1);
+    // ---- levels
     NL = 0;
     for (int c = 0; c < N; ++c) NL = std::max(NL, level[c] + 1);
     lvp.assign(NL + 1, 0);
@@ -181,6 +200,11 @@ struct KktSymbolic {
       std::vector<int32_t> fill(lvp.begin(), lvp.end() - 1);
       for (int c = 0; c < N; ++c) lvc[fill[level[c]]++] = c;
     }
+    for (int c = 0; c < N; ++c)
+      if (lvc[c] != c || (c > 0 && level[c] < level[c - 1])) {
+        error = "the level-order renumbering failed";
+        return false;
+      }
     chain0 = NL;
     while (chain0 > 0 && lvp[chain0] - lvp[chain0 - 1] == 1) --chain0;
     lep.assign(NL + 1, 0);
@@ -191,6 +215,11 @@ struct KktSymbolic {
         for (int p = Lcp[lvc[q]]; p < Lcp[lvc[q] + 1]; ++p) lee.push_back(p);
       lep[l + 1] = (int32_t)lee.size();
     }
+    for (int e = 0; e < nnzL; ++e)
+      if (lee[e] != e) {
+        error = "the level-order renumbering failed";
+        return false;
+      }
     // ---- update lists: entry (r,c) -= L(r,k) D(k) L(c,k) for k < c
     std::vector<int32_t> cnt(nnzL + 1, 0);
     auto entry = [&](int r, int c) {

@@ -2974,7 +2974,7 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
       }
   }
   std::vector<const std::vector<int32_t> *> parts = {
-      &y.pos, &y.Lcp, &y.Lri, &y.Lcl, &y.Lrp, &y.Lrc, &y.Lrq, &y.lvp, &y.lvc, &y.lep, &y.lee,
+      &y.pos, &y.Lcp, &y.Lri, &y.Lcl, &y.Lrp, &y.Lrc, &y.Lrq, &y.lvp, &y.lep,
       &y.ecp, &y.ec1, &y.ec2, &y.eck, &y.apos, &y.arow,
       &rwp, &rtb, &rln, &rbb, &rtp, &cwp, &ctb, &cln, &cbb, &ctp, &rlong, &clong, &lr, &lc};
   std::vector<size_t> off;
@@ -2997,7 +2997,7 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   if (int rc = kkt_knobs(b)) return rc;
   kd.pos = d + off[q++]; kd.Lcp = d + off[q++]; kd.Lri = d + off[q++]; kd.Lcl = d + off[q++];
   kd.Lrp = d + off[q++]; kd.Lrc = d + off[q++]; kd.Lrq = d + off[q++];
-  kd.lvp = d + off[q++]; kd.lvc = d + off[q++]; kd.lep = d + off[q++]; kd.lee = d + off[q++];
+  kd.lvp = d + off[q++]; kd.lep = d + off[q++];
   kd.ecp = d + off[q++]; kd.ec1 = d + off[q++]; kd.ec2 = d + off[q++]; kd.eck = d + off[q++];
   kd.apos = d + off[q++]; kd.arow = d + off[q++];
   Tails &tr = b->md.tr, &tc = b->md.tc;
