@@ -2709,6 +2709,7 @@ struct ph_batch {
   int mblock = 0, mpc = 0, mpr = 0;
   KktSymbolic sym;
   int32_t *d_sym = nullptr;   // every int32 array of the symbolic analysis + tails
+  uint16_t *d_sym16 = nullptr;  // the uint16 index arrays the mid polish stages in LDS
   MidArgs md{};
   int mid_lds_doubles = 0;    // LDS carve of solve_mid (doubles)
   size_t mid_lds_bytes = 0;   // LDS of the PDHG phase kernel
@@ -2947,21 +2948,49 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
                      const std::vector<int32_t> &col_ptr) {
   // PHGPU_FORCE_BIG=1: measurement hook, the big path for a mid-size shape
   const char *fb = std::getenv("PHGPU_FORCE_BIG");
-  const bool big = (fb && std::atoi(fb) != 0) || !pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr);
-  if (big) {
-    b->mblock = BIG_BLOCK;
-    b->mpc = b->mpr = 0;
-  }
+  bool big = (fb && std::atoi(fb) != 0) || !pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr);
   if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx))
     return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
                                (b->sym.error ? b->sym.error : "?"));
   const KktSymbolic &y = b->sym;
+  auto up2 = [](long v) { return (v + 1) & ~1L; };
+  auto up4 = [](long v) { return (v + 3) & ~3L; };
+  // the uint16 index arrays of the mid polish (Kkt16), each padded to 8
+  const std::vector<const std::vector<int32_t> *> p16 = {&y.pos, &y.Lcp, &y.Lri, &y.Lcl, &y.Lrp, &y.Lrc,
+                                                         &y.Lrq, &y.lvp, &y.lep, &y.ecp, &y.ec1, &y.ec2,
+                                                         &y.eck};
+  long len16 = 0;
+  for (auto *v : p16) len16 += ((long)v->size() + 7) & ~7L;
+  const bool fit16 = y.N < 65536 && y.nnzL < 65535 && y.ncontrib < 65535;
   std::vector<int32_t> rwp, rtb, rln, rbb, rtp, cwp, ctb, cln, cbb, ctp;
-  std::vector<int32_t> rlong(b->m, 0), clong(b->n, 0), lr, lc;
+  long common = 0, ws = 0;
+  bool ws_lds = false;
   if (!big) {
     build_tails(b->m, row_ptr, b->mblock, rwp, rtb, rln, rbb, rtp);
     build_tails(b->n, col_ptr.data(), b->mblock, cwp, ctb, cln, cbb, ctp);
-  } else {
+    // LDS plan (doubles): see the carve at the top of solve_mid
+    const long nw = b->mblock / WAVE;
+    auto meta = [&](long nlong) { return nw + 1 + nlong + 1 + 2 * nlong; };
+    common = up2(b->n) + up2(b->m) + MAX_WAVES * 10 + up2((long)rtp.size()) + up2((long)ctp.size()) +
+             (up4((long)rtp.size()) + up4((long)ctp.size()) + up4(meta((long)rln.size())) +
+              up4(meta((long)cln.size()))) / 2;
+    ws = up2(y.nnzL) + 3 * up2(y.N);  // the polish workspace
+    const long state = 5 * up2(b->n) + 5 * up2(b->m);  // the PDHG kernel's per-line data
+    if ((common + state + 2) * 8 > 160 * 1024)
+      return fail(PH_EINVAL, "ph_batch_create: scenario does not fit in LDS");
+    ws_lds = (common + ws + 2) * 8 + len16 * 2 <= 160 * 1024;
+    // the polish needs its uint16 index arrays in LDS: a pattern whose
+    // arrays exceed uint16 or do not fit (even with the workspace in HBM)
+    // takes the big path
+    if (!fit16 || (common + 2) * 8 + len16 * 2 > 160 * 1024) big = true;
+  }
+  if (big) {
+    b->mblock = BIG_BLOCK;
+    b->mpc = b->mpr = 0;
+    for (auto *v : {&rwp, &rtb, &rln, &rbb, &rtp, &cwp, &ctb, &cln, &cbb, &ctp}) v->clear();
+  }
+  std::vector<int32_t> rlong(b->m, 0), clong(b->n, 0), lr, lc;
+  if (big) {
     for (int i = 0; i < b->m; ++i)
       if (row_ptr[i + 1] - row_ptr[i] > BIG_LONG) {
         rlong[i] = 1;
@@ -3007,8 +3036,6 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   tc.ntail = (int)ctp.size();
   tc.wp = d + off[q++]; tc.tb = d + off[q++]; tc.ln = d + off[q++]; tc.b = d + off[q++];
   tc.tpos = d + off[q++];
-  auto up2 = [](long v) { return (v + 1) & ~1L; };
-  auto up4 = [](long v) { return (v + 3) & ~3L; };
   if (big) {
     BigArgs &g = b->bg;
     g.row_long = d + off[q++];
@@ -3028,25 +3055,46 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     b->mid_ready = false;
     return PH_OK;
   }
-  // LDS plan (doubles): see the carve at the top of solve_mid
-  const int nw = b->mblock / WAVE;
   tr.nlong = (int)rln.size();
   tc.nlong = (int)cln.size();
-  auto meta = [&](int nlong) { return (long)nw + 1 + nlong + 1 + 2L * nlong; };
-  const long common = up2(b->n) + up2(b->m) + MAX_WAVES * 10 + up2(tr.ntail) + up2(tc.ntail) +
-                      (up4(tr.ntail) + up4(tc.ntail) + up4(meta(tr.nlong)) + up4(meta(tc.nlong))) / 2;
-  const long state = 5 * up2(b->n) + 5 * up2(b->m);  // the PDHG kernel's per-line data
-  const long ws = up2(y.nnzL) + 3 * up2(y.N);         // the polish workspace
-  if ((common + state + 2) * 8 > 160 * 1024)
-    return fail(PH_EINVAL, "ph_batch_create: scenario does not fit in LDS");
+  const long state = 5 * up2(b->n) + 5 * up2(b->m);
   b->mid_lds_bytes = sizeof(double) * ((size_t)common + state + 2);
-  if ((common + ws + 2) * 8 <= 160 * 1024) {
-    b->mid_plds_bytes = sizeof(double) * ((size_t)common + ws + 2);
+  if (ws_lds) {
     b->md.ws_g = nullptr;
     b->md.ws_stride = 0;
   } else {
-    b->mid_plds_bytes = sizeof(double) * ((size_t)common + 2);
     b->md.ws_stride = ws;  // the workspace goes to HBM (allocated with the first solve)
+  }
+  // the staged uint16 arrays after the carve (and the workspace when in LDS)
+  {
+    std::vector<uint16_t> a16;
+    a16.reserve(len16);
+    std::vector<size_t> o16;
+    for (auto *v : p16) {
+      o16.push_back(a16.size());
+      for (int32_t e : *v) a16.push_back((uint16_t)e);
+      a16.resize((a16.size() + 7) & ~size_t(7), 0);
+    }
+    int rc16 = dalloc(&b->d_sym16, a16.size());
+    if (rc16) return rc16;
+    HIP_OK(hipMemcpy(b->d_sym16, a16.data(), a16.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    Kkt16 &k = b->md.k16;
+    const uint16_t *d16 = b->d_sym16;
+    k.N = y.N;
+    k.nnzL = y.nnzL;
+    k.NL = y.NL;
+    k.chain0 = y.chain0;
+    int q16 = 0;
+    k.pos = d16 + o16[q16++]; k.Lcp = d16 + o16[q16++]; k.Lri = d16 + o16[q16++]; k.Lcl = d16 + o16[q16++];
+    k.Lrp = d16 + o16[q16++]; k.Lrc = d16 + o16[q16++]; k.Lrq = d16 + o16[q16++]; k.lvp = d16 + o16[q16++];
+    k.lep = d16 + o16[q16++]; k.ecp = d16 + o16[q16++]; k.ec1 = d16 + o16[q16++]; k.ec2 = d16 + o16[q16++];
+    k.eck = d16 + o16[q16++];
+    k.apos = kd.apos;
+    k.arow = kd.arow;
+    b->md.sym16 = d16;
+    b->md.sym16_len = (int)a16.size();
+    b->md.sym16_lds = (int)(common + (ws_lds ? ws : 0) + 2);
+    b->mid_plds_bytes = sizeof(double) * (size_t)b->md.sym16_lds + sizeof(uint16_t) * a16.size();
   }
   b->mid_lds_doubles = (int)(common + state);
   b->mid_ready = true;
@@ -4069,7 +4117,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
-                  b->d_ctl, b->d_sym, b->d_ws, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
+                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ws, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
                   b->d_bws,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
