@@ -362,6 +362,12 @@ struct SolveArgs {
   const double *W, *rho, *xbar;
   double w_on, prox_on;
   double *x, *y, *omega;
+  // mid-size path: scenario-slowest copies of x [S][n] and y [S][m] and of
+  // the PH terms [S][3K] (W, rho, xbar by nonant slot), transposed around
+  // the solve (t_gather_kernel / t_scatter_kernel) so a block per scenario
+  // reads them coalesced; null: the [line][S] arrays above
+  double *xt, *yt;
+  const double *pht;
   int32_t *status, *iters;
   double *pobj, *dbound;
   double *diag;  // [S][PH_DIAG_W]: final ep, ed, eg, r, how (library-owned)
@@ -392,6 +398,49 @@ struct SolveArgs {
   unsigned long long *prof;  // [PROF_SLOTS] debug clocks and counters (ph_debug_prof), or null
   int32_t *err;              // [4] device-side invariant checks (dev_fail)
 };
+
+__device__ __forceinline__ double *x_at(const SolveArgs &a, int j, int s) {
+  return a.xt ? a.xt + (size_t)s * a.n + j : a.x + (size_t)j * a.S + s;
+}
+__device__ __forceinline__ double *y_at(const SolveArgs &a, int i, int s) {
+  return a.yt ? a.yt + (size_t)s * a.m + i : a.y + (size_t)i * a.S + s;
+}
+struct PhTerms {
+  double W, rho, xbar;
+};
+__device__ __forceinline__ PhTerms ph_terms(const SolveArgs &a, int k, int s) {
+  if (a.pht) {
+    const double *p = a.pht + (size_t)s * 3 * a.K;
+    return PhTerms{p[k], p[a.K + k], p[2 * a.K + k]};
+  }
+  const size_t o = (size_t)k * a.S + s;
+  return PhTerms{a.W[o], a.rho[o], a.xbar[o]};
+}
+
+// Tiled transposes between the [line][S] arrays and the scenario-slowest
+// copies: out[s * ld + off + r] = in[r * S + s] (gather) and back
+// (scatter), 64 x 64 tiles through LDS (coalesced on both sides).
+constexpr int TT = 64;
+__global__ void __launch_bounds__(256) t_gather_kernel(const double *__restrict__ in, int R, int S,
+                                                       double *__restrict__ out, int ld, int off) {
+  __shared__ double t[TT][TT + 1];
+  const int s0 = blockIdx.x * TT, r0 = blockIdx.y * TT, tx = threadIdx.x & (TT - 1), ty = threadIdx.x / TT;
+  for (int r = ty; r < TT; r += 4)
+    if (r0 + r < R && s0 + tx < S) t[r][tx] = in[(size_t)(r0 + r) * S + s0 + tx];
+  __syncthreads();
+  for (int q = ty; q < TT; q += 4)
+    if (s0 + q < S && r0 + tx < R) out[(size_t)(s0 + q) * ld + off + r0 + tx] = t[tx][q];
+}
+__global__ void __launch_bounds__(256) t_scatter_kernel(const double *__restrict__ in, int R, int S,
+                                                        double *__restrict__ out) {
+  __shared__ double t[TT][TT + 1];
+  const int s0 = blockIdx.x * TT, r0 = blockIdx.y * TT, tx = threadIdx.x & (TT - 1), ty = threadIdx.x / TT;
+  for (int q = ty; q < TT; q += 4)
+    if (s0 + q < S && r0 + tx < R) t[q][tx] = in[(size_t)(s0 + q) * R + r0 + tx];
+  __syncthreads();
+  for (int r = ty; r < TT; r += 4)
+    if (r0 + r < R && s0 + tx < S) out[(size_t)(r0 + r) * S + s0 + tx] = t[tx][r];
+}
 
 // Active-set polish: largest KKT system (free columns + active rows) and the
 // KKT error below which a PDHG trial point is polished.
@@ -2715,6 +2764,7 @@ struct ph_batch {
   size_t mid_lds_bytes = 0;   // LDS of the PDHG phase kernel
   size_t mid_plds_bytes = 0;  // LDS of the polish phase kernel
   double *d_ws = nullptr;     // global polish workspace (when it does not fit in LDS)
+  double *d_xt = nullptr, *d_yt = nullptr, *d_pht = nullptr;  // SolveArgs::xt / yt / pht
   int mid_grid = 0, mid_pgrid = 0;  // resident blocks of the PDHG / polish phase kernels
   int32_t *d_mlist = nullptr;  // [5][S] phase work lists
   int32_t *d_mctr = nullptr;   // [16] list counts (0..4) and queue counters (8..13)
@@ -2974,15 +3024,16 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     common = up2(b->n) + up2(b->m) + MAX_WAVES * 10 + up2((long)rtp.size()) + up2((long)ctp.size()) +
              (up4((long)rtp.size()) + up4((long)ctp.size()) + up4(meta((long)rln.size())) +
               up4(meta((long)cln.size()))) / 2;
-    ws = up2(y.nnzL) + 3 * up2(y.N);  // the polish workspace
+    ws = mid_pol_ws_len(b->n, b->m, y.nnzL, y.N);  // the polish workspace (mid_carve)
     const long state = 5 * up2(b->n) + 5 * up2(b->m);  // the PDHG kernel's per-line data
     if ((common + state + 2) * 8 > 160 * 1024)
       return fail(PH_EINVAL, "ph_batch_create: scenario does not fit in LDS");
-    ws_lds = (common + ws + 2) * 8 + len16 * 2 <= 160 * 1024;
-    // the polish needs its uint16 index arrays in LDS: a pattern whose
-    // arrays exceed uint16 or do not fit (even with the workspace in HBM)
-    // takes the big path
-    if (!fit16 || (common + 2) * 8 + len16 * 2 > 160 * 1024) big = true;
+    // the polish keeps its uint16 index arrays and the scenario's A values
+    // in LDS, the workspace too when it fits; a pattern whose arrays exceed
+    // uint16 or do not fit (even with the workspace in HBM) takes the big path
+    const long fixed = (common + up2(b->nnz) + 2) * 8 + len16 * 2;
+    ws_lds = fixed + ws * 8 <= 160 * 1024;
+    if (!fit16 || fixed > 160 * 1024) big = true;
   }
   if (big) {
     b->mblock = BIG_BLOCK;
@@ -3093,7 +3144,8 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     k.arow = kd.arow;
     b->md.sym16 = d16;
     b->md.sym16_len = (int)a16.size();
-    b->md.sym16_lds = (int)(common + (ws_lds ? ws : 0) + 2);
+    b->md.vs_lds = (int)(common + (ws_lds ? ws : 0));
+    b->md.sym16_lds = (int)(common + (ws_lds ? ws : 0) + up2(b->nnz) + 2);
     b->mid_plds_bytes = sizeof(double) * (size_t)b->md.sym16_lds + sizeof(uint16_t) * a16.size();
   }
   b->mid_lds_doubles = (int)(common + state);
@@ -3474,6 +3526,10 @@ static int mid_init(ph_batch *b) {
   }
   int rc = 0;
   if ((rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) || (rc = dalloc(&b->d_mctr, 16))) return rc;
+  // the scenario-slowest copies of x, y and the PH terms (SolveArgs::xt)
+  if ((rc = dalloc(&b->d_xt, (size_t)b->S * b->n)) || (b->m && (rc = dalloc(&b->d_yt, (size_t)b->S * b->m))) ||
+      (b->K && (rc = dalloc(&b->d_pht, (size_t)b->S * 3 * b->K))))
+    return rc;
   return PH_OK;
 }
 
@@ -3495,6 +3551,23 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   // the suspect of a mid-size graph-replay fault)
   hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_mctr, 16);
   HIP_OK(hipGetLastError());
+  const bool tr = !b->big && b->d_xt;  // the scenario-slowest copies (mid-size path)
+  auto tgrid = [&](int R) { return dim3((b->S + TT - 1) / TT, (R + TT - 1) / TT); };
+  if (tr) {
+    hipLaunchKernelGGL(t_gather_kernel, tgrid(b->n), dim3(256), 0, b->stream, a.x, b->n, b->S, b->d_xt, b->n, 0);
+    if (b->m)
+      hipLaunchKernelGGL(t_gather_kernel, tgrid(b->m), dim3(256), 0, b->stream, a.y, b->m, b->S, b->d_yt, b->m, 0);
+    if (b->K) {
+      const double *ph3[3] = {a.W, a.rho, a.xbar};
+      for (int q = 0; q < 3; ++q)
+        hipLaunchKernelGGL(t_gather_kernel, tgrid(b->K), dim3(256), 0, b->stream, ph3[q], b->K, b->S, b->d_pht,
+                           3 * b->K, q * b->K);
+    }
+    HIP_OK(hipGetLastError());
+    a.xt = b->d_xt;
+    a.yt = b->m ? b->d_yt : nullptr;
+    a.pht = b->K ? b->d_pht : nullptr;
+  }
   hipEvent_t *tev = nullptr;
   if (b->timing) {
     if (b->ev_used + 4 > b->ev.size()) {
@@ -3569,6 +3642,13 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   } else if ((rc = pdhg(in, cin, L[1], C + 1, Q + 1, 0.0, 1, 0))) {
     return rc;
   }
+  if (tr) {  // back to the [line][S] arrays (the bound pass and the PH updates read those)
+    hipLaunchKernelGGL(t_scatter_kernel, tgrid(b->n), dim3(256), 0, b->stream, b->d_xt, b->n, b->S, a.x);
+    if (b->m) hipLaunchKernelGGL(t_scatter_kernel, tgrid(b->m), dim3(256), 0, b->stream, b->d_yt, b->m, b->S, a.y);
+    HIP_OK(hipGetLastError());
+    a.xt = a.yt = nullptr;
+    a.pht = nullptr;
+  }
   // the safe outer bound of every scenario left short of the tolerance
   // (any phase; blocks of the others exit at once)
   if ((rc = launch_bound(b, a, nullptr, nullptr))) return rc;
@@ -3639,6 +3719,8 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.slot_of_col = b->d_slot_of_col;
   a.W = W; a.rho = rho; a.xbar = xbar; a.w_on = w_on; a.prox_on = prox_on;
   a.x = x; a.y = y; a.omega = omega; a.status = status; a.iters = iters;
+  a.xt = a.yt = nullptr;
+  a.pht = nullptr;
   a.pobj = pobj; a.dbound = dbound; a.diag = b->d_diag;
   a.tol = opts ? opts->tol : 1e-9;
   a.max_iters = opts ? opts->max_iters : 200000;
@@ -4117,7 +4199,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
-                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ws, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
+                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
                   b->d_bws,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
