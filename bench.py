@@ -175,6 +175,29 @@ def pmc_traffic(kname, tag):
     return None, None
 
 
+def pmc_solve_traffic(kernels, tag):
+    """HBM bytes per solve call of the listed kernels (bytes per launch x
+    launches per solve, both from the newest committed PMC summary of the
+    workload); None when the summary lacks one of them."""
+    import glob
+    if tag is None:
+        return None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary*.json")),
+                       reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != tag:
+            continue
+        ks = d.get("kernels", {})
+        if not all(k in ks and ks[k].get("hbm_bytes_per_launch") is not None for k in kernels):
+            return None
+        return round(sum(ks[k]["hbm_bytes_per_launch"] * ks[k]["launches_per_solve"] for k in kernels))
+    return None
+
+
 def _progress(msg):
     """A progress line on stderr (long profiled runs must keep writing)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -251,26 +274,27 @@ def hbm_config(args, world, farmer, PH, opts):
     dt = float(d.item())
     nt = max(n_t, 1)
     n, m, nnz = farmer_dims(c)
-    solve_ms = (k_ms + p_ms) / nt if (nk + np_) else pd_ms / nt   # all phases of one solve
+    # one solve call: the transposes into the scenario-slowest layout, the
+    # phase kernels, the transposes back and the bound pass (HIP events
+    # around the whole mid_solve launch sequence)
+    solve_ms = (as_ms + po_ms + pd_ms) / nt
     steps = st[4] / nt                                                # PDHG steps per solve call
     alg = ph.S_loc * solve_bytes_per_scenario(c)
     gbs = alg / (solve_ms / 1000.0) / 1e9
     stream_bytes = steps * bytes_per_pdhg_iter(c) + alg
     kern_ms = k_ms / max(nk, 1)
     tfs = (steps * pdhg_flops_per_step(c)) / (k_ms / nt / 1000.0) / 1e12 if k_ms > 0 else 0.0
-    trf = [pmc_traffic(k, workload_tag("farmer", ph.S_loc, c))[0]
-           for k in ("mid_kernel", "mid_polish_kernel")]
-    traffic = None
-    if all(t is not None for t in trf) and nk and np_:
-        traffic = round(trf[0] * nk / nt + trf[1] * np_ / nt)   # HBM bytes per solve call
+    traffic = pmc_solve_traffic(("t_gather_kernel", "mid_kernel", "mid_polish_kernel", "t_scatter_kernel",
+                                 "bound_kernel"), workload_tag("farmer", ph.S_loc, c))
     return {"workload": f"farmer PH, {S} scenarios ({args.scens} per GPU), crops_multiplier={c} "
                         f"(n={n}, m={m}, nnz={nnz} per scenario), rho={args.rho}",
             "value": round(S * args.hbm_steps / dt, 2), "unit": "solves/s",
             "ms_per_step": round(dt / args.hbm_steps * 1000.0, 3), "steps": args.hbm_steps,
             "iter0_s": round(t_iter0, 3), "iter0_not_optimal": nonopt0,
             "pdhg_steps_per_solve": round(st[4] / max(st[3], 1), 1), "pdhg_steps_max": st[5],
-            "roofline": {"bound": "hbm", "kernel": "mid-size solve (mid_kernel PDHG phases + "
-                                                  "mid_polish_kernel polish phases)",
+            "roofline": {"bound": "hbm", "kernel": "mid-size solve (t_gather_kernel transposes, mid_kernel "
+                                                  "PDHG phases, mid_polish_kernel polish phases, "
+                                                  "t_scatter_kernel, bound_kernel)",
                          "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "solve_ms": round(solve_ms, 3), "alg_bytes_per_solve": round(alg),
@@ -280,7 +304,7 @@ def hbm_config(args, world, farmer, PH, opts):
                                        "mid_polish_kernel": round(p_ms / max(np_, 1), 4)},
                          "note": "algorithmic bytes = each scenario's data in + solution out "
                                  "(the scenario stays on chip between PDHG steps); traffic = "
-                                 "rocprofv3 PMC bytes of the same phase launches per solve"},
+                                 "rocprofv3 PMC bytes of the same kernels per solve call"},
             "on_chip": {"bound": "fp64-vector", "kernel": "mid_kernel",
                         "flops_per_step_per_scenario": pdhg_flops_per_step(c),
                         "achieved": round(tfs, 3), "peak": FP64_VECTOR_PEAK_TFS, "unit": "TFLOP/s",

@@ -3551,6 +3551,19 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   // the suspect of a mid-size graph-replay fault)
   hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_mctr, 16);
   HIP_OK(hipGetLastError());
+  hipEvent_t *tev = nullptr;
+  if (b->timing) {
+    if (b->ev_used + 4 > b->ev.size()) {
+      for (int i = 0; i < 4; ++i) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreate(&e));
+        b->ev.push_back(e);
+      }
+    }
+    tev = &b->ev[b->ev_used];
+    b->ev_used += 4;
+    HIP_OK(hipEventRecord(tev[0], b->stream));
+  }
   const bool tr = !b->big && b->d_xt;  // the scenario-slowest copies (mid-size path)
   auto tgrid = [&](int R) { return dim3((b->S + TT - 1) / TT, (R + TT - 1) / TT); };
   if (tr) {
@@ -3567,19 +3580,6 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     a.xt = b->d_xt;
     a.yt = b->m ? b->d_yt : nullptr;
     a.pht = b->K ? b->d_pht : nullptr;
-  }
-  hipEvent_t *tev = nullptr;
-  if (b->timing) {
-    if (b->ev_used + 4 > b->ev.size()) {
-      for (int i = 0; i < 4; ++i) {
-        hipEvent_t e;
-        HIP_OK(hipEventCreate(&e));
-        b->ev.push_back(e);
-      }
-    }
-    tev = &b->ev[b->ev_used];
-    b->ev_used += 4;
-    HIP_OK(hipEventRecord(tev[0], b->stream));
   }
   int32_t *L[5], *C = b->d_mctr, *Q = b->d_mctr + 8;
   for (int i = 0; i < 5; ++i) L[i] = b->d_mlist + (size_t)i * b->S;
