@@ -28,7 +28,7 @@ ONE="--tol-run 0 --no-cpu-baseline --hbm-crops 0 --sslp-scens 0 --f4-scens 0"
 on f2 && { prof f2 20 farmer10k_c1 $ONE || exit 1; }
 on f3 && { prof f3 5 farmer10k_c100 $ONE --crops 100 --steps 5 --warmup 5 || exit 1; }
 on sslp && { prof sslp 5 sslp10k --tol-run 0 --no-cpu-baseline --hbm-crops 0 --f4-scens 0 --scens 1000 --steps 5 --warmup 5 --sslp-scens 10000 || exit 1; }
-on f4 && { prof f4 3 farmer1k_c1000 --tol-run 0 --no-cpu-baseline --hbm-crops 0 --sslp-scens 0 --scens 1000 --steps 5 --warmup 5 --f4-scens 1000 --hbm-steps 3 || exit 1; }
+on f4 && { prof f4 5 farmer1k_c1000 --tol-run 0 --no-cpu-baseline --hbm-crops 0 --sslp-scens 0 --scens 1000 --steps 5 --warmup 5 --f4-scens 1000 --hbm-steps 5 || exit 1; }
 [ "$BENCH" = bench ] || { echo ALLDONE; exit 0; }
 timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json
