@@ -29,7 +29,7 @@ lib.ph_debug_prof.restype = ctypes.c_int32
 out = np.zeros(32, dtype=np.int64)
 names = {9: "polishes", 10: "rounds", 11: "refinement solves", 12: "accepted", 1: "set repeats",
          2: "non-finite", 3: "round limit", 4: "refinement short", 6: "ep fails", 7: "ed fails",
-         8: "eg fails"}
+         8: "eg fails", 20: "repeats failing only the gap", 21: "rounds with a slack pinned row"}
 def report(tag):
     lib.ph_debug_prof(b.handle, 0, out.ctypes.data_as(ctypes.c_void_p))
     d = b.diagnostics()

@@ -42,5 +42,6 @@ print(f"per polish (block-us): setup {us(out[15])/npol:.1f} factor {us(out[13])/
       f"solves {us(out[14])/npol:.1f}")
 print(f"rounds with a pinned row {out[5]}; exits: accepted {out[12]}, set repeats {out[1]}, non-finite {out[2]}, round limit {out[3]}; "
       f"failed checks: refinement short {out[4]}, ep {out[6]}, ed {out[7]}, eg {out[8]}")
+print(f"set repeats failing only the gap {out[20]}, rounds with a slack pinned row {out[21]}")
 print(f"factorisations with a pivot held to its bound {out[16]}; non-finite: rhs {out[17]}, "
       f"refinement solve {out[18]}, check only {out[19]}")
