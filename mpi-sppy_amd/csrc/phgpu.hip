@@ -2970,10 +2970,10 @@ static int kkt_knobs(ph_batch *b) {
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_polish_rounds), &r, sizeof(r)));
     }
   }
-  {  // PHGPU_MID_PIN=0: measurement hook, no pinned rows in the mid-size polish
+  {  // PHGPU_MID_PIN=0: measurement hook, no pinned rows in the mid-size polish (2: slack test)
     const char *e = std::getenv("PHGPU_MID_PIN");
     if (e) {
-      const int v = std::atoi(e) != 0;
+      const int v = std::max(0, std::min(2, std::atoi(e)));
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_pin_rows), &v, sizeof(v)));
     }
   }

@@ -36,6 +36,10 @@ def report(tag):
     st = b.status.cpu().numpy()
     print(tag, {v: int(out[k]) for k, v in names.items()}, "how", np.bincount(d[:, 4].astype(int), minlength=4),
           "not optimal", int((st != 0).sum()), flush=True)
+    if out[22]:  # the first gap-only failure's decomposition (polish_big debug slots 23..29)
+        g = out[23:30].copy().view(np.float64)
+        print("  gap-only failure: free cols %.3e fixed cols %.3e active rows %.3e inactive rows %.3e "
+              "pobj %.9e dobj %.9e eg %.3e" % tuple(g), flush=True)
 lib.ph_debug_prof(b.handle, 1, None)
 ph.Iter0()
 report("Iter0")
