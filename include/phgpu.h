@@ -174,6 +174,23 @@ int ph_eval_objective(ph_batch_t b, const double *x, const double *W,
                       double prox_on, double *obj);
 
 /*
+ * Bundles (phbase.py:803-862 FormEF / 1273-1302 subproblem_creation;
+ * sputils.py:246-383 _create_EF_from_scen_dict): a bundle is ONE batched
+ * subproblem (its scenarios' blocks plus nonanticipativity rows), so the
+ * bundle batch's PH terms are gathered from the scenario batch's [K][S]
+ * W / rho / xbar with the EF objective's weights p_s / P_b (sputils.py:
+ * 314-322), and the bundle solution goes back to the scenarios' [n][S] x
+ * (the reference's scenario sub-blocks "naturally get the EF solution",
+ * phbase.py:833-838).  One indexed gather on the batch's stream:
+ *   dst[e] = wt[e] * src[idx[e]]   (wt NULL: 1;  idx[e] < 0: 0),  e < count.
+ * src: dev [src_count]; idx: dev int32 [count]; wt: dev [count] or NULL;
+ * dst: dev [count].  An index >= src_count is a device-side check failure
+ * (PH_EDEV at the next synchronising call) and reads 0.
+ */
+int ph_gather(ph_batch_t b, const double *src, int64_t src_count, const int32_t *idx,
+              const double *wt, int64_t count, double *dst);
+
+/*
  * Diagnostics of the last ph_pdhg_solve, copied to host out[PH_DIAG_W*S]:
  * per scenario the final relative primal residual, dual residual, duality
  * gap, Halpern fixed-point residual and how the solve ended (0 PDHG reached

@@ -316,6 +316,7 @@ enum DevCheck : int32_t {
   CHK_ENTRY_RANGE = 3,    // a list entry outside [0, S) (v0 = entry, v1 = list index)
   CHK_WS_RANGE = 4,       // a block past the HBM polish workspace (v0 = block, v1 = slices)
   CHK_QUEUE_RANGE = 5,    // a queue ticket below the grid (v0 = index, v1 = grid)
+  CHK_GATHER_RANGE = 6,   // a ph_gather index past its source (v0 = index, v1 = element)
 };
 __device__ __forceinline__ void dev_fail(int32_t *err, int code, int v0, int v1) {
   if (err && atomicCAS(err, 0, code) == 0) {
@@ -1258,6 +1259,7 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
   double LAM[CPT];  // scaled reduced costs of the last KKT evaluation
   int how = 0;      // 0: PDHG reached tol, 1: polished at start, 2: polished mid-solve
   int nchk = 0;     // KKT checks (the infeasibility test runs on every fourth)
+  int cert_prev = -1;  // the previous infeasibility test's outcome
 
   // Local KKT terms of the trial point (XN, YN, AXN), unscaled; ys must hold
   // YN.  v[0..5] = primal residual^2, dual residual^2, primal objective,
@@ -1537,8 +1539,12 @@ __device__ __forceinline__ void solve_scenario(const SolveArgs &a, const int s, 
         if (i < m) ray_terms_row(ys[i], RL[b], RU[b], DOT[b], rv);
       }
       block_sum<6>(rv, red);
+      // a certificate counts once two consecutive tests agree (advisor r3:
+      // one test was enough to stop a large-valued feasible model)
       const int cert = ray_status(rv);
-      if (cert >= 0) {
+      const bool certified = cert >= 0 && cert == cert_prev;
+      cert_prev = cert;
+      if (certified) {
         stat = cert;
         ++it;
         break;
@@ -2948,10 +2954,11 @@ static int check_dev(const int32_t (&e)[4]) {
   if (e[0] == 0) return PH_OK;
   static const char *what[] = {"?", "work list pushed past its capacity S",
                                "work-list count above S", "work-list entry outside [0, S)",
-                               "block past the HBM polish workspace", "work-queue ticket out of range"};
+                               "block past the HBM polish workspace", "work-queue ticket out of range",
+                               "gather index past its source array"};
   char msg[256];
   std::snprintf(msg, sizeof(msg), "device-side check failed: %s (code %d, values %d %d)",
-                what[(e[0] >= 1 && e[0] <= 5) ? e[0] : 0], e[0], e[1], e[2]);
+                what[(e[0] >= 1 && e[0] <= 6) ? e[0] : 0], e[0], e[1], e[2]);
   return fail(PH_EDEV, msg);
 }
 
@@ -2968,6 +2975,13 @@ static int kkt_knobs(ph_batch *b) {
     if (e) {
       const int r = std::max(1, std::atoi(e));
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_polish_rounds), &r, sizeof(r)));
+    }
+  }
+  {  // PHGPU_BIG_POLISH_ROUNDS: PDAS rounds of one big-path polish
+    const char *e = std::getenv("PHGPU_BIG_POLISH_ROUNDS");
+    if (e) {
+      const int r = std::max(1, std::atoi(e));
+      HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_big_polish_rounds), &r, sizeof(r)));
     }
   }
   {  // PHGPU_MID_PIN=0: measurement hook, no pinned rows in the mid-size polish (2: slack test)
@@ -3661,6 +3675,25 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   return PH_OK;
 }
 
+// Bundles (phbase.py:803-862 FormEF, :1273-1302): the bundle batch's PH
+// terms are gathered from the scenario batch's [K][S] arrays weighted by
+// p_s / P_b (the EF objective's normalisation, sputils.py:314-322), and the
+// bundle solution goes back to the scenarios' [n][S] x -- both one indexed
+// gather: dst[e] = wt[e] * src[idx[e]] (wt NULL: 1; idx < 0: 0).  An index
+// past the source is recorded (CHK_GATHER_RANGE) and reads 0.
+__global__ void __launch_bounds__(256) gather_kernel(const double *__restrict__ src, long src_count,
+                                                     const int32_t *__restrict__ idx,
+                                                     const double *__restrict__ wt, long count,
+                                                     double *__restrict__ dst, int32_t *err) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < count; e += (long)gridDim.x * 256) {
+    const int32_t i = idx[e];
+    double v = 0.0;
+    if (i >= 0 && i < src_count) v = src[i];
+    else if (i >= src_count) dev_fail(err, CHK_GATHER_RANGE, i, (int)e);
+    dst[e] = wt ? wt[e] * v : v;
+  }
+}
+
 // The one-wave path without the active-set cache (Iter0, cold or bound
 // solves): pdhg_kernel over every scenario, then the rescue polish of the
 // ones it left at the iteration limit (its list) and their safe bounds.
@@ -3902,6 +3935,18 @@ int ph_eval_objective(ph_batch_t b, const double *x, const double *W, const doub
   if (b->K && (!W || !rho || !xbar)) return fail(PH_EINVAL, "ph_eval_objective: null W/rho/xbar");
   hipLaunchKernelGGL(eval_obj_kernel, dim3((b->S + 255) / 256), dim3(256), 0, b->stream, b->S,
                      b->n, b->d_c, b->d_slot_of_col, x, W, rho, xbar, w_on, prox_on, obj);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+int ph_gather(ph_batch_t b, const double *src, int64_t src_count, const int32_t *idx,
+              const double *wt, int64_t count, double *dst) {
+  if (!b || !src || !idx || !dst || count < 0 || src_count < 0 || src_count > INT32_MAX)
+    return fail(PH_EINVAL, "ph_gather: bad arguments");
+  if (count == 0) return PH_OK;
+  const long grid = std::min<long>((count + 255) / 256, 65536);
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)grid), dim3(256), 0, b->stream, src, (long)src_count, idx,
+                     wt, (long)count, dst, b->d_err);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }

@@ -59,6 +59,7 @@ SIGNATURES = [
                              _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
     ("ph_segment_sum", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_int, _c_ptr, _c_ptr]),
     ("ph_eval_objective", _c_int, [_c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_dbl, _c_dbl, _c_ptr]),
+    ("ph_gather", _c_int, [_c_ptr, _c_ptr, ctypes.c_int64, _c_ptr, _c_ptr, ctypes.c_int64, _c_ptr]),
     ("ph_batch_get_diag", _c_int, [_c_ptr, _c_ptr]),
     ("ph_batch_solve_summary", _c_int, [_c_ptr, _c_ptr]),
     ("ph_loop_reset", _c_int, [_c_ptr, _c_int, _c_int, _c_dbl]),

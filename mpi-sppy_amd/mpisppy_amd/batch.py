@@ -371,6 +371,11 @@ class DeviceBatch:
         _native.check(self.lib.ph_segment_sum(self.handle, _native.ptr(v), _native.ptr(w), R,
                                               _native.ptr(seg), _native.ptr(out)), "ph_segment_sum")
 
+    def gather(self, src, idx, wt, count, dst):
+        """dst[e] = wt[e] * src[idx[e]] on the batch's stream (ph_gather)."""
+        _native.check(self.lib.ph_gather(self.handle, _native.ptr(src), int(src.numel()), _native.ptr(idx),
+                                         _native.ptr(wt), int(count), _native.ptr(dst)), "ph_gather")
+
     def eval_objective(self, W, rho, xbar, w_on, prox_on, out):
         _native.check(self.lib.ph_eval_objective(self.handle, _native.ptr(self.x), _native.ptr(W),
                                                  _native.ptr(rho), _native.ptr(xbar), float(w_on),

@@ -15,6 +15,7 @@ import math
 import time
 import warnings
 
+import contextlib
 import numpy as np
 import torch
 
@@ -27,6 +28,10 @@ _PDHG_KEYS = {"pdhg_tol": "tol", "pdhg_max_iters": "max_iters",
               "pdhg_reflection": "reflection", "pdhg_polish": "polish"}
 _DEFAULT_SOLVE = dict(tol=1e-9, max_iters=200000, check_every=64, warm_start=True,
                       reflection=1.0, polish=True)
+
+
+def _nullctx():
+    return contextlib.nullcontext()
 
 
 class PHBase(SPBase):
@@ -233,7 +238,13 @@ class PHBase(SPBase):
         self._set_flags()
 
     def subproblem_creation(self, verbose=False):
-        """phbase.py:1273-1302 (no bundles: subproblems are the scenarios)."""
+        """phbase.py:1273-1302: the subproblems are the scenarios, or with
+        bundles_per_rank the bundles (formed at SPBase construction as one
+        batched layout, bundles.BundleLayout)."""
+        if self.bundling and verbose and self.cylinder_rank == 0:
+            for bname, bv in self.local_subproblems.items():
+                for sname in bv.scen_list:
+                    print("bundling " + sname + " into " + bname)
         self.subproblems_created = True
 
     def _create_solvers(self):
@@ -249,7 +260,66 @@ class PHBase(SPBase):
             stream = torch.cuda.Stream(self.device)
             stream.wait_stream(torch.cuda.current_stream(self.device))
         self.batch = DeviceBatch(self.batch_data, device=self.device, stream=stream)
+        if self.bundling:
+            self._create_bundle_batch(stream)
         self.set_instance_time = time.time() - t0
+
+    def _create_bundle_batch(self, stream, batch_factory=None):
+        """Bundles (phbase.py:1273-1302, 803-862): the rank's bundle
+        subproblems as a second device batch (bundles.BundleLayout) with the
+        index maps of its PH-term gather and solution scatter.
+        (batch_factory: a test's CPU stand-in instead of DeviceBatch.)"""
+        from .batch import DeviceBatch
+        bl = self.bundle_layout
+        dev = self.device
+        self.bbatch = DeviceBatch(bl.data, device=dev, stream=stream) if batch_factory is None \
+            else batch_factory(bl.data)
+        f64 = dict(dtype=torch.float64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self._b_term_idx = torch.as_tensor(bl.term_idx, **i32)
+        self._b_term_wt = torch.as_tensor(bl.term_wt, **f64)
+        self._b_x_idx = torch.as_tensor(bl.x_idx, **i32)
+        nt = bl.term_idx.size
+        self._b_W = torch.zeros(nt, **f64)
+        self._b_rho = torch.zeros(nt, **f64)
+        self._b_xbar = torch.zeros(nt, **f64)
+        self._b_prob = torch.as_tensor(bl.P, **f64)
+        self._b_seg = torch.tensor([0, bl.Sb], **i32)
+        self._b_of = torch.as_tensor(bl.bundle_of, dtype=torch.int64, device=dev)
+        self._b_scal = torch.zeros(1, **f64)
+
+    def _launch_solve(self, kw):
+        """Queue the batched solve of every local subproblem.  With bundles:
+        the bundle batch's PH terms gathered from the scenario arrays with
+        the EF weights p_s / P_b, the bundle solve, and its solution
+        scattered to the scenarios' x (the scenario sub-blocks hold the EF
+        solution, phbase.py:833-838); one ph_gather call per array."""
+        if not self.bundling:
+            self.batch.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
+            return
+        bb = self.bbatch
+        nt = self._b_term_idx.numel()
+        for src, dst, wt in ((self.W, self._b_W, self._b_term_wt), (self.rho, self._b_rho, self._b_term_wt),
+                             (self.xbar, self._b_xbar, None)):
+            bb.gather(src, self._b_term_idx, wt, nt, dst)
+        bb.solve(self._b_W, self._b_rho, self._b_xbar, self.w_on, self.prox_on, **kw)
+        bb.gather(bb.x, self._b_x_idx, None, self._b_x_idx.numel(), self.batch.x)
+
+    def _solve_summary(self):
+        """(not optimal, PDHG iterations sum, max, polished, cached) of the
+        last solve (waits for it); with bundles the bundle solve's, and the
+        bundle statuses copied to their scenarios (phbase.py:992-995)."""
+        if not self.bundling:
+            return self.batch.summary()
+        out = self.bbatch.summary()
+        ts = getattr(self.batch, "torch_stream", None)
+        with torch.cuda.stream(ts) if ts is not None else _nullctx():
+            self.batch.status.copy_(self.bbatch.status.index_select(0, self._b_of))
+        return out
+
+    @property
+    def n_subproblems(self):
+        return self.bundle_layout.Sb if self.bundling else self.S_loc
 
     # ----------------------------------------------------------- solves --
     def solve_loop_launch(self, solver_options=None, dis_W=False, dis_prox=False):
@@ -266,7 +336,7 @@ class PHBase(SPBase):
             self._create_solvers()
         kw = self._solve_kwargs(solver_options)
         self._launch_t0 = time.perf_counter()
-        self.batch.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
+        self._launch_solve(kw)
         # (the flags were read at launch)
         if dis_W and dis_prox:
             self._reenable_W_and_prox()
@@ -279,10 +349,10 @@ class PHBase(SPBase):
     def solve_loop_finish(self, kw, gripe=False):
         """The host half of solve_loop: wait for the solve, statuses ->
         scenario_feasible (phbase.py:959-989)."""
-        nonopt, it_sum, it_max, npol, ncache = self.batch.summary()  # waits for the solve
+        nonopt, it_sum, it_max, npol, ncache = self._solve_summary()  # waits for the solve
         dt = time.perf_counter() - self._launch_t0
-        self.solve_log.append((self.S_loc, dt, it_sum / max(self.S_loc, 1), it_max,
-                               npol + ncache))
+        ns = self.n_subproblems
+        self.solve_log.append((ns, dt, it_sum / max(ns, 1), it_max, npol + ncache))
         self._set_feasibility(nonopt, gripe, kw["max_iters"])
 
     def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False,
@@ -298,13 +368,12 @@ class PHBase(SPBase):
         if self.batch is None:
             self._create_solvers()
         kw = self._solve_kwargs(solver_options)
-        b = self.batch
         t0 = time.perf_counter()
-        b.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
-        nonopt, it_sum, it_max, npol, ncache = b.summary()  # waits for the solve
+        self._launch_solve(kw)
+        nonopt, it_sum, it_max, npol, ncache = self._solve_summary()  # waits for the solve
         dt = time.perf_counter() - t0
-        self.solve_log.append((self.S_loc, dt, it_sum / max(self.S_loc, 1), it_max,
-                               npol + ncache))
+        ns = self.n_subproblems
+        self.solve_log.append((ns, dt, it_sum / max(ns, 1), it_max, npol + ncache))
         self._set_feasibility(nonopt, gripe, kw["max_iters"])
         if dtiming:
             allt = self.comm.allgather_object(dt)
@@ -333,6 +402,10 @@ class PHBase(SPBase):
         if nonopt:
             status = self.batch.status.cpu().numpy()
             self.scenario_feasible = status <= 1
+            sub_names = self.local_scenario_names
+            if self.bundling:  # the reference gripes per subproblem (phbase.py:959-978)
+                status = self.bbatch.status.cpu().numpy()
+                sub_names = self.bundle_layout.names
         elif not self._all_feasible:
             self.scenario_feasible = np.ones(self.S_loc, dtype=bool)
         self._all_feasible = not nonopt
@@ -349,12 +422,13 @@ class PHBase(SPBase):
         # them with verbose)
         bad = np.nonzero(status != 0)[0]
         show = bad if self.PHoptions.get("verbose", False) else bad[:5]
+        what = "bundle" if self.bundling else "scenario"
         for i in show:
-            print(f"[{name}] Solve failed for scenario {self.local_scenario_names[i]}: "
+            print(f"[{name}] Solve failed for {what} {sub_names[i]}: "
                   f"{why.get(int(status[i]), 'status %d' % status[i])}")
         if len(show) < len(bad):
             print(f"[{name}] ... {len(bad) - len(show)} more failed solves "
-                  f"({len(bad)} of {self.S_loc} local scenarios)")
+                  f"({len(bad)} of {len(status)} local {what}s)")
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -415,9 +489,18 @@ class PHBase(SPBase):
         return ob if self.is_minimizing else -ob
 
     def Ebound(self, verbose=False, extra_sum_terms=None):
-        """phbase.py:314-354: sum_s p_s * outer_bound_s (+ extra terms)."""
-        ob = self._outer_bounds().contiguous()
-        t = self._weighted_sum(ob).clone()
+        """phbase.py:314-354: sum over subproblems of probability x
+        outer_bound (+ extra terms); a bundle's probability is the sum of its
+        scenarios' (phbase.py:1297-1298)."""
+        if self.bundling:
+            bb = self.bbatch
+            ob = bb.dbound + bb.const
+            ob = (ob if self.is_minimizing else -ob).contiguous()
+            bb.segment_sum(ob, self._b_prob, self._b_seg, self._b_scal)
+            t = self._b_scal.clone()
+        else:
+            ob = self._outer_bounds().contiguous()
+            t = self._weighted_sum(ob).clone()
         if extra_sum_terms is not None:
             t = torch.cat([t, torch.tensor(list(extra_sum_terms), dtype=torch.float64,
                                            device=t.device)])
@@ -444,6 +527,8 @@ class PHBase(SPBase):
     def _save_nonants(self):
         """phbase.py _save_nonants: the current nonant values of every local
         scenario (device copy)."""
+        if self.bundling:  # (phbase.py:451-455: not on bundles in the reference either)
+            raise RuntimeError("_save_nonants called for a bundle")
         cols = torch.as_tensor(self.batch_data.nonant_cols.astype(np.int64), device=self.device)
         self._saved_nonant_cols = cols
         self._saved_nonants = self.batch.x.view(self.batch.n, self.S_loc).index_select(0, cols).clone()
@@ -451,6 +536,8 @@ class PHBase(SPBase):
     def _fix_nonants(self, xhat_slots):
         """phbase.py _fix_nonants: every local scenario's nonants fixed at the
         node-slot values xhat_slots [G] (l = u on the nonant columns)."""
+        if self.bundling:
+            raise RuntimeError("_fix_nonants called for a bundle")
         b = self.batch
         n, S = b.n, self.S_loc
         vals = torch.as_tensor(np.asarray(xhat_slots, dtype=np.float64)[self.gid_host],
@@ -574,7 +661,7 @@ class PHBase(SPBase):
         when nothing on the host has to see each iteration (no extensions,
         converger, hub/spoke communicator or per-iteration printing)."""
         o = self.PHoptions
-        return (o.get("device_loop", True) and self.PH_extensions is None
+        return (o.get("device_loop", True) and self.PH_extensions is None and not self.bundling
                 and self.PH_converger is None
                 and (self.spcomm is None or hasattr(self.spcomm, "sync_every"))
                 and not o["display_progress"] and not o["display_convergence_detail"]

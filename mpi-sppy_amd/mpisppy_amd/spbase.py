@@ -71,14 +71,15 @@ class SPBase:
         global_toc("Initializing SPBase")
         if self.n_proc > len(self.all_scenario_names):
             raise RuntimeError("More ranks than scenarios")
-        if "bundles_per_rank" in options and options["bundles_per_rank"]:
-            raise NotImplementedError("bundles_per_rank > 0: bundling is not on the batched hot path")
-        self.bundling = False
+        self.names_in_bundles = None
+        self.bundling = bool(options.get("bundles_per_rank", 0))
         if "branching_factors" in options:
             self.branching_factors = options["branching_factors"]
         else:
             self.branching_factors = [len(self.all_scenario_names)]
         self._calculate_scenario_ranks()
+        if self.bundling:
+            self._assign_bundles()
         self._create_scenarios(scenario_creator_kwargs)
         self._look_and_leap()
         self._compute_unconditional_node_probabilities()
@@ -86,6 +87,7 @@ class SPBase:
         self._verify_nonant_lengths()
         self.is_minimizing = self.batch_data.sense == "min"
         self._use_variable_probability_setter(options.get("verbose", False))
+        self.bundle_layout = self._form_bundles() if self.bundling else None
         self._spcomm = None
 
     # ---------------------------------------------------------------- setup
@@ -96,6 +98,24 @@ class SPBase:
         self.local_scenario_names = [self.all_scenario_names[i] for i in self.local_scenario_indices]
         self.local_begin = self.local_scenario_indices[0]
         self.local_end = self.local_scenario_indices[-1] + 1
+
+    def _assign_bundles(self):
+        """spbase.py:206-240: names_in_bundles[rank][bundle] = [scenario names]."""
+        from .bundles import assign_bundles
+        bpr = int(self.options["bundles_per_rank"])
+        if self.options.get("verbose", False) and self.cylinder_rank == 0:
+            print("(rank0)", bpr, "bundles per rank")
+        self.names_in_bundles = assign_bundles(self._rank_slices, self.all_scenario_names, bpr)
+
+    def _form_bundles(self):
+        """phbase.py:1273-1302 + 803-862: this rank's bundles as ONE batched
+        layout of bundle subproblems (:class:`bundles.BundleLayout`)."""
+        from .bundles import BundleLayout
+        idx = {nm: i for i, nm in enumerate(self.local_scenario_names)}
+        mine = self.names_in_bundles[self.cylinder_rank]
+        groups = [[idx[nm] for nm in mine[b]] for b in sorted(mine)]
+        names = [f"rank{self.cylinder_rank}bundle{b}" for b in sorted(mine)]
+        return BundleLayout(self.batch_data, groups, self.local_prob, self.gid_host, names)
 
     def _create_scenarios(self, scenario_creator_kwargs):
         kw = {} if scenario_creator_kwargs is None else dict(scenario_creator_kwargs)
@@ -299,7 +319,17 @@ class SPBase:
 
     @property
     def local_subproblems(self):
-        return self.local_scenarios
+        """phbase.py:1273-1302: the scenarios, or with bundles the bundles
+        (name, scen_list, _mpisppy_probability)."""
+        if not self.bundling:
+            return self.local_scenarios
+        if not hasattr(self, "_bundle_views"):
+            from .bundles import BundleView
+            bl = self.bundle_layout
+            mine = self.names_in_bundles[self.cylinder_rank]
+            self._bundle_views = {nm: BundleView(nm, mine[b], bl.P[b])
+                                  for b, nm in enumerate(bl.names)}
+        return self._bundle_views
 
     @property
     def spcomm(self):

@@ -22,8 +22,12 @@ def rank_slices(num_scens, n_proc):
 class OraclePH:
     """PH over a list of :class:`oracle.models.OScen` (all scenarios, in order)."""
 
-    def __init__(self, options, scens, n_proc=1, variable_prob=None):
+    def __init__(self, options, scens, n_proc=1, variable_prob=None, bundles=None):
         self.options = dict(options)
+        # bundles: lists of scenario indices solved as one EF subproblem
+        # (spbase.py:206-240, phbase.py:803-862 / 1273-1302); None: each
+        # scenario is a subproblem
+        self.bundles = None if bundles is None else [list(b) for b in bundles]
         self.scens = scens
         self.S = len(scens)
         self.n_proc = n_proc
@@ -96,10 +100,67 @@ class OraclePH:
         return v if self.is_min else -v
 
     # -------------------------------------------------------------- solve --
+    def _solve_bundle(self, b, members, w_on, prox_on):
+        """One bundle: the EF of its scenarios (sputils.py:246-383) -- the
+        PH-augmented scenario objectives weighted by p_s and normalised by the
+        bundle probability P_b, nonanticipativity rows x_s[k] == x_ref[k]
+        per tree node (ref: the bundle's first scenario at the node) -- solved
+        exactly; every member gets its block of the solution, the bundle its
+        outer bound (phbase.py:985-995)."""
+        import scipy.sparse as sp
+        P = float(sum(self.prob[s] for s in members))
+        gs, qs, cst = [], [], 0.0
+        for s in members:
+            g, q, c0 = self._terms(s, w_on, prox_on)
+            wt = self.prob[s] / P
+            gs.append(wt * g)
+            qs.append(wt * q)
+            cst += wt * c0
+        ns = [self.scens[s].A.shape[1] for s in members]
+        offs = np.concatenate([[0], np.cumsum(ns)]).astype(int)
+        A = sp.block_diag([self.scens[s].A for s in members], format="csr")
+        rl = [np.concatenate([self.scens[s].rl for s in members])]
+        ru = [np.concatenate([self.scens[s].ru for s in members])]
+        first = {}
+        link = []
+        for t, s in enumerate(members):
+            for (nm, cp, idx) in self.scens[s].nodes:
+                if nm not in first:
+                    first[nm] = (t, idx)
+                    continue
+                t0, idx0 = first[nm]
+                for a, r in zip(idx, idx0):
+                    link.append((offs[t] + a, offs[t0] + r))
+        if link:
+            na = sp.csr_matrix((np.tile([1.0, -1.0], len(link)),
+                                (np.repeat(np.arange(len(link)), 2), np.array(link).reshape(-1))),
+                               shape=(len(link), offs[-1]))
+            A = sp.vstack([A, na]).tocsr()
+            rl.append(np.zeros(len(link)))
+            ru.append(np.zeros(len(link)))
+        g, q = np.concatenate(gs), np.concatenate(qs)
+        l = np.concatenate([self.scens[s].l for s in members])
+        u = np.concatenate([self.scens[s].u for s in members])
+        x, y, feas = solve_scenario(g, q, A, np.concatenate(rl), np.concatenate(ru), l, u)
+        for t, s in enumerate(members):
+            self.feasible[s] = feas
+            if feas:
+                self.x[s] = x[offs[t]:offs[t + 1]].copy()
+        if feas:
+            v = 0.5 * float(np.dot(q * x, x)) + float(np.dot(g, x)) + cst
+            self.bundle_bound[b] = v if self.is_min else -v
+        self.solve_count += 1
+
     def solve_loop(self, w_on=None, prox_on=None):
         """phbase.py:999-1095 + solve_one 864-996."""
         w_on = self.w_on if w_on is None else w_on
         prox_on = self.prox_on if prox_on is None else prox_on
+        if self.bundles is not None:
+            if not hasattr(self, "bundle_bound"):
+                self.bundle_bound = np.zeros(len(self.bundles))
+            for b, members in enumerate(self.bundles):
+                self._solve_bundle(b, members, w_on, prox_on)
+            return
         for s in range(self.S):
             sc = self.scens[s]
             g, q, const = self._terms(s, w_on, prox_on)
@@ -161,7 +222,10 @@ class OraclePH:
         return math.fsum(self.prob[s] * self.objective(s) for s in range(self.S))
 
     def Ebound(self):
-        """phbase.py:314-354."""
+        """phbase.py:314-354 (over subproblems: a bundle weighs P_b)."""
+        if self.bundles is not None:
+            return math.fsum(float(sum(self.prob[s] for s in mem)) * self.bundle_bound[b]
+                             for b, mem in enumerate(self.bundles))
         return math.fsum(self.prob[s] * self.outer_bound[s] for s in range(self.S))
 
     # ------------------------------------------------------------ drivers --

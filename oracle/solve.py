@@ -337,6 +337,20 @@ def _pdas(x0, c, q, A, rl, ru, l, u, tau, kkt_tol, rounds=20):
     return best
 
 
+def _checked_vertex(x, rowdual, c, q, A, rl, ru, l, u, kkt_tol):
+    """HiGHS' simplex vertex with the row-dual sign that passes the KKT
+    check (HiGHS reports d(obj)/d(activity); the oracle's y > 0 means a row
+    at rl), or OracleSolveError when neither sign does."""
+    best = None
+    for y in (rowdual, -rowdual):
+        err = max(kkt_residual(x, y, c, q, A, rl, ru, l, u))
+        if best is None or err < best[0]:
+            best = (err, y)
+    if best[0] > kkt_tol:
+        raise OracleSolveError(f"simplex vertex fails the KKT check: residual {best[0]:.3e}")
+    return x, best[1], True
+
+
 def solve_scenario(c, q, A, rl, ru, l, u, kkt_tol=1e-9):
     """Solve min 1/2 x'diag(q)x + c'x s.t. rl<=Ax<=ru, l<=x<=u exactly.
 
@@ -390,8 +404,8 @@ def solve_scenario(c, q, A, rl, ru, l, u, kkt_tol=1e-9):
     large = A.shape[0] + A.shape[1] > DENSE_MAX
     if not np.any(q) and large:
         # a large LP's simplex vertex is exact to its tolerances (the dense
-        # polish below is for small degenerate QP/LP cases)
-        return x, rowdual, True
+        # polish below is for small degenerate QP/LP cases): verified
+        return _checked_vertex(x, rowdual, c, q, A, rl, ru, l, u, kkt_tol)
     for tau in (1e-7, 1e-8, 1e-6, 1e-9, 1e-5, 1e-10, 1e-4):
         if large:
             break
@@ -404,7 +418,7 @@ def solve_scenario(c, q, A, rl, ru, l, u, kkt_tol=1e-9):
             return xp, yp, True
     if not np.any(q):
         # an LP vertex from simplex is already exact to its tolerances
-        return x, rowdual, True
+        return _checked_vertex(x, rowdual, c, q, A, rl, ru, l, u, kkt_tol)
     # degenerate LP parts (many free columns without a prox term): the
     # tolerance guess of the active set is off -- primal-dual active-set
     # iterations from it, as the GPU polish does

@@ -233,6 +233,11 @@ class CPUBatch:
             a, b = int(seg[r]), int(seg[r + 1])
             out[r] = (v[a:b] * (w[a:b] if w is not None else 1.0)).sum()
 
+    def gather(self, src, idx, wt, count, dst):
+        i = idx.long()
+        v = torch.where(i >= 0, src[i.clamp(min=0)], torch.zeros_like(dst))
+        dst.copy_(v * wt if wt is not None else v)
+
     def eval_objective(self, W, rho, xbar, w_on, prox_on, out):
         d = self.data
         X = self.x.view(self.n, self.S)

@@ -412,3 +412,109 @@ def test_three_rank_gloo_doc_farmer_config1():
            ("bad", "X[CORN]"): 85.26131687116226}
     for k, r in ref.items():
         assert abs(v[k] - r) / abs(r) < 1e-8, (k, v[k], r)
+
+
+def test_bundle_assignment_matches_reference_slicing():
+    """spbase.py:206-240: each rank's scenarios cut into bundles_per_rank
+    contiguous slices range(int(i*avg), int((i+1)*avg)); too many bundles
+    is an error."""
+    from mpisppy_amd.bundles import assign_bundles
+    from mpisppy_amd.utils.sputils import rank_slices
+    names = [f"scen{i}" for i in range(11)]
+    nb = assign_bundles(rank_slices(11, 2), names, 2)
+    assert nb[0] == {0: ["scen0", "scen1"], 1: ["scen2", "scen3", "scen4"]}
+    assert nb[1] == {0: ["scen5", "scen6", "scen7"], 1: ["scen8", "scen9", "scen10"]}
+    with pytest.raises(RuntimeError, match="Not enough scenarios"):
+        assign_bundles(rank_slices(11, 2), names, 6)
+
+
+def test_bundle_layout_is_the_bundles_extensive_form():
+    """Each bundle of the batched layout (bundles.BundleLayout: T blocks of
+    the scenario pattern + chained nonanticipativity rows, an inert pad
+    block for a short bundle) solved as an LP equals oracle/ef.py's EF of
+    its scenarios (star nonanticipativity rows, sputils.py:246-383), both
+    with the scenarios' probabilities: P_b x bound_b == EF value."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    from oracle.ef import solve_ef
+    import scipy.sparse as sp
+    from oracle.solve import solve_scenario
+    names = [f"scen{i}" for i in range(11)]
+    ph = PH(_opts(bundles_per_rank=4), names, farmer.scenario_creator)
+    bl = ph.bundle_layout
+    assert bl.T == 3 and bl.Sb == 4
+    assert [len(v.scen_list) for v in ph.local_subproblems.values()] == [2, 3, 3, 3]
+    d = bl.data
+    for b, (bname, bv) in enumerate(ph.local_subproblems.items()):
+        A = sp.csr_matrix((d.vals[:, b], d.col_idx, d.row_ptr), shape=(d.m, d.n))
+        x, y, feas = solve_scenario(d.c[:, b], None, A, d.rl[:, b], d.ru[:, b], d.l[:, b], d.u[:, b])
+        assert feas
+        val = bl.P[b] * (float(d.c[:, b] @ x) + float(d.const[b]))
+        scens = [om.farmer(nm) for nm in bv.scen_list]
+        for sc in scens:
+            sc.prob = 1.0 / len(names)
+        ef, _ = solve_ef(scens)
+        assert abs(val - ef) <= 1e-9 * abs(ef), (b, val, ef)
+
+
+@pytest.mark.parametrize("S,bpr", [(12, 4), (11, 3)])
+def test_bundled_ph_host_flow_matches_oracle(S, bpr):
+    """PH with bundles_per_rank (phbase.py:1273-1302, 803-862, 985-995) on
+    the CPU stand-in: the bundle batch's PH terms gathered with p_s / P_b,
+    its solution scattered to the scenarios; trivial bound (bundle EF
+    values), W, x-bar, conv and Eobj against the oracle PH on the same
+    bundles."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    from cpu_batch import CPUBatch
+    names = [f"scen{i}" for i in range(S)]
+    opts = _opts(PHIterLimit=8, bundles_per_rank=bpr)
+    ph = PH(dict(opts), names, farmer.scenario_creator)
+    ph.batch = CPUBatch(ph.batch_data)
+    ph._create_bundle_batch(None, batch_factory=CPUBatch)
+    conv, eobj, tb = ph.ph_main()
+    idx = {nm: i for i, nm in enumerate(names)}
+    bundles = [[idx[nm] for nm in bv.scen_list] for bv in ph.local_subproblems.values()]
+    orc = OraclePH(dict(opts), [om.farmer(n) for n in names], bundles=bundles)
+    oc, oe, ot = orc.ph_main()
+    assert ph._PHIter == orc.iters
+    assert abs(tb - ot) < 1e-9 * abs(ot)
+    assert abs(eobj - oe) < 1e-8 * abs(oe)
+    assert abs(conv - oc) < 1e-7 * abs(oc)
+    W = ph.W.view(ph.K, ph.S_loc).numpy().T
+    assert np.allclose(W, np.array(orc.W), rtol=1e-7, atol=1e-7)
+    # the bundles' trivial bound is at least the scenarios' (a bundle is a
+    # relaxation of fewer nonanticipativity constraints dropped)
+    orc1 = OraclePH(dict(opts), [om.farmer(n) for n in names])
+    assert tb >= orc1.Iter0() - 1e-9 * abs(tb)
+
+
+def test_bundled_hydro_multistage_matches_oracle():
+    """Bundles across tree nodes (hydro, 9 scenarios in 2 bundles: the first
+    holds ROOT_0's three scenarios and one of ROOT_1): the chained
+    nonanticipativity rows are active only between blocks of the same node
+    at each slot; trivial bound, Eobj and conv against the oracle's star EF
+    bundles."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import hydro
+    from cpu_batch import CPUBatch
+    names, nodes = hydro.all_names_and_nodes()
+    opts = _opts(PHIterLimit=10, convthresh=1e-3, branching_factors=[3, 3], bundles_per_rank=2)
+    ph = PH(dict(opts), names, hydro.scenario_creator, all_nodenames=nodes,
+            scenario_creator_kwargs={"branching_factors": [3, 3]})
+    ph.batch = CPUBatch(ph.batch_data)
+    ph._create_bundle_batch(None, batch_factory=CPUBatch)
+    conv, eobj, tb = ph.ph_main()
+    assert [len(v.scen_list) for v in ph.local_subproblems.values()] == [4, 5]
+    bl = ph.bundle_layout
+    K = ph.K
+    # block 3 of bundle 0 is Scen4 (ROOT_1): ROOT slots linked, ROOT_0/ROOT_1 slots not
+    lrl = bl.data.rl[bl.T * ph.batch_data.m:, 0].reshape(bl.T - 1, K)
+    assert np.all(lrl[2, :4] == 0.0) and np.all(np.isinf(lrl[2, 4:]))
+    assert np.all(lrl[1] == 0.0)
+    orc = OraclePH(dict(opts), [om.hydro(nm) for nm in names], bundles=[[0, 1, 2, 3], [4, 5, 6, 7, 8]])
+    oc, oe, ot = orc.ph_main()
+    assert ph._PHIter == orc.iters
+    assert abs(tb - ot) < 1e-9 * abs(ot)
+    assert abs(eobj - oe) < 1e-7 * abs(oe)
+    assert abs(conv - oc) < 1e-6 * abs(oc)
