@@ -528,6 +528,10 @@ def _parser():
     ap.add_argument("--f4-crops", type=int, default=1000)
     ap.add_argument("--sslp-scens", type=int, default=10000,
                     help="scenarios per rank of the sslp companion config (BASELINE config 5); 0 = skip")
+    ap.add_argument("--only", choices=["f3", "f4", "sslp"], default=None,
+                    help="profiling: run ONLY this companion config, exactly as the full line runs "
+                         "it (its timed window is then the last --hbm-steps solve calls of the "
+                         "process, the window tools/pmc_summary.py reads); prints its JSON")
     return ap
 
 
@@ -572,6 +576,17 @@ def run():
     from mpisppy_amd.examples import farmer
 
     S, c = args.scens * world, args.crops  # weak scaling: --scens per rank
+    if args.only:
+        o1 = {"solvername": "mi355x_pdhg", "PHIterLimit": 100000, "defaultPHrho": args.rho,
+              "convthresh": -1.0, "verbose": False, "display_progress": False,
+              "display_timing": False, "iter0_solver_options": {}, "iterk_solver_options": {},
+              "device_loop_graphs": False}
+        res = {"f3": lambda: hbm_config(args, world, farmer, PH, o1),
+               "f4": lambda: big_config(args, world, farmer, PH, o1),
+               "sslp": lambda: sslp_config(args, world, PH, o1)}[args.only]()
+        if world > 1:
+            dist.destroy_process_group()
+        return {"only": args.only, args.only: res} if rank == 0 else None
     names = [f"scen{i}" for i in range(S)]
     opts = {"solvername": "mi355x_pdhg", "PHIterLimit": args.warmup + args.steps,
             "defaultPHrho": args.rho, "convthresh": -1.0, "verbose": False,

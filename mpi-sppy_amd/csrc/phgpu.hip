@@ -422,8 +422,12 @@ __device__ __forceinline__ PhTerms ph_terms(const SolveArgs &a, int k, int s) {
 // copies: out[s * ld + off + r] = in[r * S + s] (gather) and back
 // (scatter), 64 x 64 tiles through LDS (coalesced on both sides).
 constexpr int TT = 64;
+// (both return at once on a stopped device loop: a stopped pass's phases do
+// nothing, so its round trip would only move bytes)
 __global__ void __launch_bounds__(256) t_gather_kernel(const double *__restrict__ in, int R, int S,
-                                                       double *__restrict__ out, int ld, int off) {
+                                                       double *__restrict__ out, int ld, int off,
+                                                       const LoopCtl *ctl) {
+  if (stopped(ctl)) return;
   __shared__ double t[TT][TT + 1];
   const int s0 = blockIdx.x * TT, r0 = blockIdx.y * TT, tx = threadIdx.x & (TT - 1), ty = threadIdx.x / TT;
   for (int r = ty; r < TT; r += 4)
@@ -433,7 +437,8 @@ __global__ void __launch_bounds__(256) t_gather_kernel(const double *__restrict_
     if (s0 + q < S && r0 + tx < R) out[(size_t)(s0 + q) * ld + off + r0 + tx] = t[tx][q];
 }
 __global__ void __launch_bounds__(256) t_scatter_kernel(const double *__restrict__ in, int R, int S,
-                                                        double *__restrict__ out) {
+                                                        double *__restrict__ out, const LoopCtl *ctl) {
+  if (stopped(ctl)) return;
   __shared__ double t[TT][TT + 1];
   const int s0 = blockIdx.x * TT, r0 = blockIdx.y * TT, tx = threadIdx.x & (TT - 1), ty = threadIdx.x / TT;
   for (int q = ty; q < TT; q += 4)
@@ -3581,14 +3586,16 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   const bool tr = !b->big && b->d_xt;  // the scenario-slowest copies (mid-size path)
   auto tgrid = [&](int R) { return dim3((b->S + TT - 1) / TT, (R + TT - 1) / TT); };
   if (tr) {
-    hipLaunchKernelGGL(t_gather_kernel, tgrid(b->n), dim3(256), 0, b->stream, a.x, b->n, b->S, b->d_xt, b->n, 0);
+    hipLaunchKernelGGL(t_gather_kernel, tgrid(b->n), dim3(256), 0, b->stream, a.x, b->n, b->S, b->d_xt, b->n, 0,
+                       a.ctl);
     if (b->m)
-      hipLaunchKernelGGL(t_gather_kernel, tgrid(b->m), dim3(256), 0, b->stream, a.y, b->m, b->S, b->d_yt, b->m, 0);
+      hipLaunchKernelGGL(t_gather_kernel, tgrid(b->m), dim3(256), 0, b->stream, a.y, b->m, b->S, b->d_yt, b->m, 0,
+                         a.ctl);
     if (b->K) {
       const double *ph3[3] = {a.W, a.rho, a.xbar};
       for (int q = 0; q < 3; ++q)
         hipLaunchKernelGGL(t_gather_kernel, tgrid(b->K), dim3(256), 0, b->stream, ph3[q], b->K, b->S, b->d_pht,
-                           3 * b->K, q * b->K);
+                           3 * b->K, q * b->K, a.ctl);
     }
     HIP_OK(hipGetLastError());
     a.xt = b->d_xt;
@@ -3657,8 +3664,9 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     return rc;
   }
   if (tr) {  // back to the [line][S] arrays (the bound pass and the PH updates read those)
-    hipLaunchKernelGGL(t_scatter_kernel, tgrid(b->n), dim3(256), 0, b->stream, b->d_xt, b->n, b->S, a.x);
-    if (b->m) hipLaunchKernelGGL(t_scatter_kernel, tgrid(b->m), dim3(256), 0, b->stream, b->d_yt, b->m, b->S, a.y);
+    hipLaunchKernelGGL(t_scatter_kernel, tgrid(b->n), dim3(256), 0, b->stream, b->d_xt, b->n, b->S, a.x, a.ctl);
+    if (b->m)
+      hipLaunchKernelGGL(t_scatter_kernel, tgrid(b->m), dim3(256), 0, b->stream, b->d_yt, b->m, b->S, a.y, a.ctl);
     HIP_OK(hipGetLastError());
     a.xt = a.yt = nullptr;
     a.pht = nullptr;

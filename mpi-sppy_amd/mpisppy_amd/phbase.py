@@ -414,21 +414,26 @@ class PHBase(SPBase):
         name = type(self).__name__
         if self.spcomm is not None:
             name = type(self.spcomm).__name__
-        why = {1: f"PDHG iteration limit ({max_iters}) reached before the KKT tolerance "
-                  "(kept as feasible, safe outer bound)",
-               2: "primal infeasible (certificate)", 3: "dual infeasible, unbounded (certificate)"}
-        # the reference prints one line per failed solve (phbase.py:959-978);
-        # a batch of 10k scenarios prints the first few and a count (all of
-        # them with verbose)
-        bad = np.nonzero(status != 0)[0]
-        show = bad if self.PHoptions.get("verbose", False) else bad[:5]
+        why = {2: "primal infeasible (certificate)", 3: "dual infeasible, unbounded (certificate)"}
         what = "bundle" if self.bundling else "scenario"
+        # the reference prints one line per infeasible / unbounded solve
+        # (phbase.py:959-978); a batch of 10k scenarios prints the first few
+        # and a count (all of them with verbose)
+        bad = np.nonzero(status >= 2)[0]
+        show = bad if self.PHoptions.get("verbose", False) else bad[:5]
         for i in show:
             print(f"[{name}] Solve failed for {what} {sub_names[i]}: "
                   f"{why.get(int(status[i]), 'status %d' % status[i])}")
         if len(show) < len(bad):
             print(f"[{name}] ... {len(bad) - len(show)} more failed solves "
                   f"({len(bad)} of {len(status)} local {what}s)")
+        # an iteration-limit stop is silent in the reference (a solver's
+        # maxIterations termination loads its point as feasible): a count
+        # with verbose only
+        nlim = int(np.sum(status == 1))
+        if nlim and self.PHoptions.get("verbose", False):
+            print(f"[{name}] {nlim} of {len(status)} local {what}s stopped at the PDHG iteration "
+                  f"limit ({max_iters}) short of the KKT tolerance (kept as feasible, safe outer bound)")
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -780,7 +785,12 @@ class PHBase(SPBase):
         eager) on a CUDA device.  With one ph_loop_pass call per iteration
         the eager loop issues in ~21 us against ~60 us of GPU work per F2
         iteration, and measured faster than the graph replay
-        (profiles/r03: 0.0601 / 0.0612 against 0.0629 / 0.0658 ms per step)."""
+        (profiles/r03: 0.0601 / 0.0612 against 0.0629 / 0.0658 ms per step).
+        Replay of mid-size and big-path chunks is EXPERIMENTAL: round 2's
+        intermittent mid-size replay fault was not caught in the act (its
+        presumed cause, the chunked summary's stop race, was removed and
+        device-side checks now turn a recurrence into PH_EDEV),
+        so keep the option off outside tests and measurements."""
         b = self.batch
         return (self.PHoptions.get("device_loop_graphs", False) and self.comm.size == 1
                 and self.device.type == "cuda" and hasattr(b, "set_stream"))

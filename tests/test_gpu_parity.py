@@ -903,3 +903,43 @@ def test_bundled_ph_matches_oracle(model):
     assert _rel(W, np.array(orc.W)) < 1e-5
     xb = ph.xbar.view(ph.K, ph.S_loc).cpu().numpy().T
     assert _rel(xb, np.array(orc.xbar)) < 1e-5
+
+
+def test_wxbar_files_from_the_hip_path_match_oracle_and_resume(tmp_path):
+    """SURVEY 8 f-3 on the HIP path (utils/wxbarutils.py:40-79, 264-284 via
+    the WXBarWriter / WXBarReader extensions): a GPU PH on farmer S=12 writes
+    W (rows sname,vname,W) and x-bar (vname,xbar) after 10 iterations; the
+    rows equal the oracle PH's W / x-bar to 1e-5.  A fresh GPU PH initialised
+    from the files (its Iter0 solves with those W / x-bar, as the reference's
+    reader re-enables W and prox) and run 4 iterations reproduces the
+    uninterrupted 14-iteration run's W and x-bar."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    from mpisppy_amd.utils.wxbarwriter import WXBarWriter
+    from mpisppy_amd.utils.wxbarreader import WXBarReader
+    names = [f"scen{i}" for i in range(12)]
+    wf, xf = str(tmp_path / "w.csv"), str(tmp_path / "x.csv")
+    ph = PH(_opts(PHIterLimit=10, convthresh=-1.0, W_fname=wf, Xbar_fname=xf), names,
+            farmer.scenario_creator, PH_extensions=WXBarWriter)
+    ph.ph_main()
+    orc = OraclePH(_opts(PHIterLimit=10, convthresh=-1.0), [om.farmer(n) for n in names])
+    orc.ph_main()
+    pnames = ph.nonant_names()
+    rows = [ln.rsplit(",", 1) for ln in open(wf).read().strip().split("\n")]
+    assert len(rows) == 12 * ph.K
+    Wf = np.zeros((12, ph.K))
+    for (key, val) in rows:
+        sname, vname = key.split(",", 1)
+        Wf[names.index(sname), pnames.index(vname)] = float(val)
+    assert _rel(Wf, np.array(orc.W)) < 1e-5
+    xrows = dict(ln.rsplit(",", 1) for ln in open(xf).read().strip().split("\n"))
+    xbf = np.array([float(xrows[v]) for v in pnames])
+    assert _rel(xbf, orc.xbar[0]) < 1e-5
+    # resume from the files
+    ph2 = PH(_opts(PHIterLimit=4, convthresh=-1.0, init_W_fname=wf, init_Xbar_fname=xf), names,
+             farmer.scenario_creator, PH_extensions=WXBarReader)
+    ph2.ph_main()
+    ph3 = PH(_opts(PHIterLimit=14, convthresh=-1.0), names, farmer.scenario_creator)
+    ph3.ph_main()
+    assert _rel(ph2.W.cpu().numpy(), ph3.W.cpu().numpy()) < 1e-6
+    assert _rel(ph2.xbar.cpu().numpy(), ph3.xbar.cpu().numpy()) < 1e-6

@@ -24,7 +24,9 @@ the round-2 profiles):
   sslp10k         mid_kernel<512, 2, 1> / mid_polish_kernel<512, 2, 1> only
                   (n = 705, m = 60)
 
-Window: the launches after the (WINDOW+1)-th last `summary_kernel` dispatch,
+Window "first": the launches up to the first `summary_kernel` dispatch (the
+Iter0 solve, e.g. F4's streaming PDHG).
+Window N: the launches after the (N+1)-th last `summary_kernel` dispatch,
 i.e. the last WINDOW solve calls (one summary kernel closes each solve) --
 the eagerly launched PH iterations whose HIP-event times give the bench
 line's `achieved`, so traffic and algorithmic bytes describe the same
@@ -82,20 +84,25 @@ def _rows(d, pattern):
     return rows
 
 
-def _window_start(rows, window):
-    """Dispatch id after which the last `window` solve calls start."""
+def _window(rows, window):
+    """(first, last] dispatch ids of the window: the last `window` solve
+    calls, or with window "first" the process's first solve call (Iter0)."""
     summ = sorted({int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "summary_kernel"})
+    if window == "first":
+        if not summ:
+            raise SystemExit("pmc_summary: no solve call recorded")
+        return -1, summ[0]
     if len(summ) <= window:
         raise SystemExit(f"pmc_summary: only {len(summ)} solve calls recorded, window {window}")
-    return summ[-window - 1]
+    return summ[-window - 1], 1 << 62
 
 
 def per_kernel(d, counter, window):
     rows = [r for r in _rows(d, "*counter_collection.csv") if r["Counter_Name"] == counter]
-    w0 = _window_start(rows, window)
+    w0, w1 = _window(rows, window)
     vals, meta, inst = {}, {}, {}
     for r in rows:
-        if int(r["Dispatch_Id"]) <= w0:
+        if not (w0 < int(r["Dispatch_Id"]) <= w1):
             continue
         k = short(r["Kernel_Name"])
         vals.setdefault(k, []).append(float(r["Counter_Value"]))
@@ -127,16 +134,18 @@ def validate(tag, res, inst):
 
 def main():
     fd, wd, sd, outp, tag = sys.argv[1:6]
-    window = int(sys.argv[6]) if len(sys.argv) > 6 else 20
+    window = sys.argv[6] if len(sys.argv) > 6 else "20"
+    window = "first" if window == "first" else int(window)
+    nsolve = 1 if window == "first" else window
     if tag not in WORKLOADS:
         raise SystemExit(f"pmc_summary: unknown workload {tag}; one of {sorted(WORKLOADS)}")
     fetch, meta, inst = per_kernel(fd, "FETCH_SIZE", window)
     write, _, _ = per_kernel(wd, "WRITE_SIZE", window)
     trows = _rows(sd, "*kernel_trace.csv")
-    w0 = _window_start(trows, window)
+    w0, w1 = _window(trows, window)
     times = {}
     for r in trows:
-        if int(r["Dispatch_Id"]) <= w0:
+        if not (w0 < int(r["Dispatch_Id"]) <= w1):
             continue
         times.setdefault(short(r["Kernel_Name"]), []).append(
             int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
@@ -146,19 +155,22 @@ def main():
                      "--kernel-trace --stats of the bench command",
            "fetch_correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section)",
            "scenarios_per_rank": wl["scenarios_per_rank"], "crops_multiplier": wl["crops_multiplier"],
-           "window": f"launches of the last {window} solve calls (after the "
-                     f"{window + 1}-th last summary_kernel dispatch)",
+           "window": ("launches of the process's first solve call (Iter0)" if window == "first" else
+                      f"launches of the last {window} solve calls (after the "
+                      f"{window + 1}-th last summary_kernel dispatch)"),
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         fk, nf = fetch.get(k, (None, 0))
         wk, _ = write.get(k, (None, 0))
         t = times.get(k, [])
-        hbm = None
+        hbm = raw = None
         if fk is not None and wk is not None:
             hbm = round((2.0 * fk + wk) * 1024.0)
+            raw = round((fk + wk) * 1024.0)
         res["kernels"][k] = {"instances": sorted(inst.get(k, [])),
                              "fetch_kB_raw": fk, "write_kB": wk, "hbm_bytes_per_launch": hbm,
-                             "launches_per_solve": round(nf / window, 3),
+                             "hbm_bytes_per_launch_uncorrected": raw,
+                             "launches_per_solve": round(nf / nsolve, 3),
                              "mean_ns": (sum(t) / len(t)) if t else None, **meta.get(k, {})}
     validate(tag, res, inst)
     with open(outp, "w") as f:
