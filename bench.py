@@ -111,7 +111,8 @@ def cpu_subproblem_rate(c, sample_scens, min_seconds=10.0, cores=16):
                       f"x {dtm:.1f} s ({nm} solves)"}
 
 
-def cpu_baseline(c, scens, convthresh, cores=16, f3_crops=100, f3_sample=64, f3_seconds=8.0):
+def cpu_baseline(c, scens, convthresh, cores=16, f3_crops=100, f3_sample=64, f3_seconds=8.0,
+                 n1_iters=50):
     """the oracle PH (oracle/ph_dist.py: phbase.py's
     Iter0/iterk control flow, exact HiGHS + KKT-polish subproblem solves,
     Compute_Xbar/convergence_diff allreduces) on `cores` gloo ranks of this
@@ -136,12 +137,43 @@ def cpu_baseline(c, scens, convthresh, cores=16, f3_crops=100, f3_sample=64, f3_
            "ph_to_tol": {"seconds": round(r["seconds_to_tol"], 3), "ph_iterations": r["iterations"],
                          "scenarios": scens, "convthresh": convthresh, "final_conv": r["conv"],
                          "Eobj": r["Eobj"], "trivial_bound": r["trivial_bound"]}}
+    # N=1: the same run on one rank, bounded to n1_iters PH
+    # iterations (about 10 s of CPU work at ~1.2k solves/s)
+    try:
+        t1 = time.perf_counter()
+        r1 = ph_dist.run(1, scens, crops=c, rho=1.0, convthresh=convthresh, limit=n1_iters)
+        out["n1"] = {"value": round(r1["subproblem_solves"] / r1["seconds_to_tol"], 2), "unit": "solves/s",
+                     "cores": 1, "sample": f"the same oracle PH on 1 rank, {scens} scenarios, Iter0 + "
+                                           f"{r1['iterations']} PH iterations ({r1['subproblem_solves']} "
+                                           f"solves in {r1['seconds_to_tol']:.2f} s; "
+                                           f"{time.perf_counter() - t1:.1f} s with start-up)"}
+    except Exception as e:
+        out["n1"] = {"value": None, "error": repr(e)}
+    out["host"] = host_cpu_info()
     if f3_crops > 0:
         try:
             out["f3_subproblems"] = cpu_subproblem_rate(f3_crops, f3_sample, f3_seconds, cores)
         except Exception as e:  # the F3 sample must not kill the baseline
             out["f3_subproblems"] = {"value": None, "error": repr(e)}
     return out
+
+
+def host_cpu_info():
+    """lscpu of the host the CPU baseline ran on (record N and
+    lscpu) and the CPUs this process may use."""
+    import subprocess
+    info = {"affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    try:
+        txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        keep = ("Model name", "CPU(s)", "Thread(s) per core", "Core(s) per socket", "Socket(s)",
+                "NUMA node(s)", "CPU max MHz", "L3 cache")
+        for ln in txt.splitlines():
+            k, _, v = ln.partition(":")
+            if k.strip() in keep:
+                info[k.strip()] = v.strip()
+    except Exception as e:  # lscpu missing: say so
+        info["lscpu_error"] = repr(e)
+    return info
 
 
 def workload_tag(kind, S_loc, c=None):
@@ -751,7 +783,12 @@ def run():
             "ms_per_step": round(dt / args.steps * 1000.0, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": (round(value / cpu["value"], 1) if cpu and cpu.get("value") else None),
+            "vs_baseline_basis": "value / cpu_baseline.value: the oracle PH (exact HiGHS subproblem "
+                                 "solves, no Pyomo overhead) on the GPU box's host, cpu_baseline.cores "
+                                 "gloo ranks, a 200-scenario sample of the same farmer workload "
+                                 "(BASELINE.md section 2's CPU baseline; the reference publishes no "
+                                 "number for this metric)",
             "dtype": "f64",
             "data": "synthetic (reference farmer generator, examples/farmer/farmer.py)",
             "config": {"workload": f"farmer PH, {S} scenarios ({args.scens} per GPU), crops_multiplier={c} "

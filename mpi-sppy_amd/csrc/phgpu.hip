@@ -2788,6 +2788,7 @@ struct ph_batch {
   double *d_vals_t = nullptr;   // [S][nnz] CSC-ordered scaled values
   double *d_bws = nullptr;      // workspace slices
   size_t big_lds_bytes = 0;     // LDS of big_kernel (y + scratch)
+  bool big_ylds = true;         // big_kernel<true>: y in LDS; <false>: y in the slice (m > ~20,000)
   int big_grid = 0;             // resident blocks of the big phase kernels
 };
 
@@ -3117,8 +3118,8 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     // LDS: scratch + queue slot + y [m]; the slice: the larger of the PDHG
     // and polish layouts (and the scaling's vectors)
     b->big_lds_bytes = sizeof(double) * ((size_t)MAX_WAVES * 10 + 2 + up2(b->m));
-    if (b->big_lds_bytes > 160 * 1024)
-      return fail(PH_EINVAL, "ph_batch_create: more than 20,000 rows; the big path keeps y in LDS");
+    b->big_ylds = b->big_lds_bytes <= 160 * 1024;
+    if (!b->big_ylds) b->big_lds_bytes = BIG_SMALL_LDS;  // y in the workspace slice
     g.ws_stride = std::max({big_pdhg_ws_len(b->n, b->m), big_pol_ws_len(b->n, b->m, y.nnzL, y.N),
                             2 * up2(b->n) + up2(b->m)});
     b->big = true;
@@ -3486,9 +3487,13 @@ static int big_init(ph_batch *b) {
   int per_cu = 0, per_cu_p = 0, cus = 0, dev = 0;
   HIP_OK(hipGetDevice(&dev));
   HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  HIP_OK(hipFuncSetAttribute((const void *)big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)b->big_lds_bytes));
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, big_kernel, BIG_BLOCK, b->big_lds_bytes));
+  if (b->big_ylds) {
+    HIP_OK(hipFuncSetAttribute((const void *)big_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)b->big_lds_bytes));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, big_kernel<true>, BIG_BLOCK, b->big_lds_bytes));
+  } else {
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, big_kernel<false>, BIG_BLOCK, b->big_lds_bytes));
+  }
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, big_polish_kernel, BIG_BLOCK,
                                                       BIG_SMALL_LDS));
   if (per_cu < 1 || per_cu_p < 1) return fail(PH_EINVAL, "ph_batch_bind: the big-path kernels cannot be resident");
@@ -3609,8 +3614,12 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     const MidPhase ph{in, cin, out, cout, q, exit_err, first, 0, hand_at_limit};
     if (int rc = phase_event(b, 0)) return rc;
     if (b->big) {
-      hipLaunchKernelGGL(big_kernel, dim3(b->big_grid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream, a,
-                         b->bg, ph);
+      if (b->big_ylds)
+        hipLaunchKernelGGL(big_kernel<true>, dim3(b->big_grid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
+                           a, b->bg, ph);
+      else
+        hipLaunchKernelGGL(big_kernel<false>, dim3(b->big_grid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
+                           a, b->bg, ph);
       HIP_OK(hipGetLastError());
       return phase_event(b, -1);
     }

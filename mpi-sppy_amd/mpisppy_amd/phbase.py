@@ -607,18 +607,19 @@ class PHBase(SPBase):
                 print(f"  {sn:>20s} {vn:>30s} {val:.6f}")
 
     def _use_rho_setter(self, verbose):
-        """phbase.py:556-588: rho_setter(model) -> [(vardata, rho)] per scenario."""
+        """phbase.py:556-588: rho_setter(scenario) -> [(var, rho)] per
+        scenario; var is a nonant VarData of the scenario's model, its id()
+        (the reference's form) or a nonant variable name (batched scenarios
+        without per-scenario models get their ScenarioView)."""
         if self.rho_setter is None:
             return
         models = self.batch_data.models
-        if models is None:
-            raise RuntimeError("rho_setter needs per-scenario models (per_scenario_models=True)")
-        from . import repn
-        col2k = {int(c): k for k, c in enumerate(self.batch_data.nonant_cols)}
         rho = self.rho.view(self.K, self.S_loc)
-        for s, mdl in enumerate(models):
-            for vd, r in self.rho_setter(mdl):
-                rho[col2k[repn.column_of(mdl, vd)], s] = float(r)
+        views = list(self.local_scenarios.values())
+        for s in range(self.S_loc):
+            target = models[s] if models is not None else views[s]
+            for key, r in self.rho_setter(target):
+                rho[self._nonant_slot_of(s, key), s] = float(r)
 
     # ----------------------------------------------------------- drivers --
     def Iter0(self):

@@ -289,3 +289,233 @@ def sslp(scenario_name, instance="sslp_15_45_5"):
              + [f"Dummy[{j + 1}]" for j in range(J)])
     nodes = [("ROOT", 1.0, list(yo))]
     return OScen(scenario_name, names, c, sp.csr_matrix(A), rl, ru, l, u, nodes)
+
+
+# ------------------------------------------------------------------- uc -----
+# paperruns/larger_uc/ReferenceModel_OK.py (the egret-free, Pyomo-only unit
+# commitment model; uc_funcs.py builds egret's "tight" model instead), its
+# LP relaxation (binaries in [0, 1]), restated from the model's rules on the
+# WECC-240 data of paperruns/larger_uc (tools/make_uc_data.py):
+# regulation_services = reserve_services = False, storage_services = True
+# with no storage units, one bus, no lines, WIND nondispatchable.
+# The reference states PiecewiseProductionCostsConstr once per piece with
+# the same body (ReferenceModel_OK.py:1454-1458); the rows are identical, so
+# the restatement keeps one per (g, t): same feasible set and objective.
+_UC_JSON = None
+
+
+def _uc_json():
+    global _UC_JSON
+    if _UC_JSON is None:
+        import json
+        import os
+        here = os.path.dirname(os.path.abspath(__file__))
+        path = os.path.join(here, "..", "mpi-sppy_amd", "mpisppy_amd", "examples", "data", "uc_wecc240.json")
+        with open(path) as f:
+            _UC_JSON = json.load(f)
+    return _UC_JSON
+
+
+def _uc_piecewise(pts, vals, pmin, pmax):
+    """ReferenceModel_OK.py:530-585 (points/values are ordered Pyomo Sets:
+    duplicates dropped; sorted; min / max output added; clipped; values cut
+    or extended by +1, +2, ...)."""
+    def uniq(v):
+        out = []
+        for a in v:
+            if a not in out:
+                out.append(a)
+        return out
+    p = sorted(uniq(pts))
+    v = sorted(uniq(vals))
+    if pmin not in p:
+        p.insert(0, pmin)
+    if pmax not in p:
+        p.append(pmax)
+    p = [a for a in p if pmin <= a <= pmax]
+    if len(p) < len(v):
+        v = v[:len(p)]
+    i = 1
+    while len(p) > len(v):
+        v.append(v[-1] + i)
+        i += 1
+    return p, v
+
+
+def uc(scenario_name, scenario_set="1000scenarios_wind"):
+    """One UC scenario's LP relaxation (ScenarioN -> NodeN's wind)."""
+    d = _uc_json()
+    snum = extract_num(scenario_name)
+    T = int(d["NumTimePeriods"])
+    TPL = float(d["TimePeriodLength"])
+    gens = list(d["ThermalGenerators"])
+    wind_lo = np.asarray(d["scenario_sets"][scenario_set]["wind_min"][snum - 1])
+    wind_hi = np.asarray(d["scenario_sets"][scenario_set]["wind_max"][snum - 1])
+    cols = {}          # name -> index
+    lo, hi, cost = [], [], []
+
+    def var(name, l_, u_, c_=0.0):
+        cols[name] = len(lo)
+        lo.append(l_)
+        hi.append(u_)
+        cost.append(c_)
+        return cols[name]
+
+    rows_r, rows_c, rows_v, rl, ru = [], [], [], [], []
+
+    def row(terms, l_, u_):
+        r = len(rl)
+        acc = {}
+        for j, a in terms:
+            acc[j] = acc.get(j, 0.0) + a
+        for j, a in acc.items():
+            if a != 0.0:
+                rows_r.append(r)
+                rows_c.append(j)
+                rows_v.append(a)
+        rl.append(l_)
+        ru.append(u_)
+
+    INF = np.inf
+    on, st, sp_, pg, mp = {}, {}, {}, {}, {}
+    pc, suc, sdc, si, pp = {}, {}, {}, {}, {}
+    par = {}
+    for g in gens:
+        t_ = d["gen_table"][g]
+        pmin, pmax = t_["MinimumPowerOutput"], t_["MaximumPowerOutput"]
+        fuel = t_["FuelCost"]
+        pts, vals = _uc_piecewise(d["piecewise_points"][g], d["piecewise_values"][g], pmin, pmax)
+        minprod = vals[0] * fuel if len(pts) > 1 else 0.0
+        pwp = [a - pmin for a in pts]
+        pwv = [b - minprod / fuel for b in vals]
+        t0 = t_["UnitOnT0State"]
+        u0 = 1 if t0 >= 1 else 0
+        mu = min(int(round(t_["MinimumUpTime"] / TPL)), T)
+        md = min(int(round(t_["MinimumDownTime"] / TPL)), T)
+        on_init = 0 if not u0 else int(min(T, round(max(0, t_["MinimumUpTime"] - t0) / TPL)))
+        off_init = 0 if u0 else int(min(T, round(max(0, t_["MinimumDownTime"] + t0) / TPL)))
+        lags = list(d["startup_lags"][g])
+        scost = list(d["startup_costs"][g])
+        vstp = list(range(1, T + 1)) + ([] if t0 >= 0 else [1 + int(t0)])
+        pairs = [(tp, tt) for tp in vstp for tt in range(1, T + 1) if lags[0] <= tt - tp < lags[-1]]
+        par[g] = dict(pmin=pmin, pmax=pmax, fuel=fuel, pwp=pwp, pwv=pwv, minprod=minprod, u0=u0, mu=mu,
+                      md=md, on_init=on_init, off_init=off_init, lags=lags, scost=scost, vstp=vstp,
+                      pairs=pairs, pg0=t_["PowerGeneratedT0"],
+                      rup=min(t_["NominalRampUpLimit"] * TPL, pmax),
+                      rdn=min(t_["NominalRampDownLimit"] * TPL, pmax),
+                      sul=min(t_["StartupRampLimit"], pmax), sdl=min(t_["ShutdownRampLimit"], pmax),
+                      mut=int(t_["MinimumUpTime"]))
+        for t in range(1, T + 1):
+            on[g, t] = var(f"UnitOn[{g},{t}]", 0.0, 1.0, minprod * TPL)
+            st[g, t] = var(f"UnitStart[{g},{t}]", 0.0, 1.0)
+            sp_[g, t] = var(f"UnitStop[{g},{t}]", 0.0, 1.0)
+            pg[g, t] = var(f"PowerGeneratedAboveMinimum[{g},{t}]", 0.0, pmax - pmin)
+            mp[g, t] = var(f"MaximumPowerAvailableAboveMinimum[{g},{t}]", 0.0, pmax - pmin)
+            pc[g, t] = var(f"ProductionCost[{g},{t}]", 0.0, INF, 1.0)
+            suc[g, t] = var(f"StartupCost[{g},{t}]", 0.0, INF, 1.0)
+            sdc[g, t] = var(f"ShutdownCost[{g},{t}]", 0.0, INF, 1.0)
+            for i in range(len(pwp) - 1):
+                pp[g, t, i] = var(f"PiecewiseProduction[{g},{t},{i}]", 0.0, pwp[i + 1] - pwp[i])
+        for (tp, tt) in pairs:
+            si[g, tp, tt] = var(f"StartupIndicator[{g},{tp},{tt}]", 0.0, 1.0)
+    nd = {t: var(f"NondispatchablePowerUsed[WIND,{t}]", wind_lo[t - 1], wind_hi[t - 1]) for t in range(1, T + 1)}
+    ang = {t: var(f"Angle[SingleBus,{t}]", -3.14159265, 3.14159265) for t in range(1, T + 1)}
+    tpc = {t: var(f"TotalProductionCost[{t}]", 0.0, INF) for t in range(1, T + 1)}
+    tnl = {t: var(f"TotalNoLoadCost[{t}]", 0.0, INF) for t in range(1, T + 1)}
+    lgm = {t: var(f"LoadGenerateMismatch[SingleBus,{t}]", -INF, INF) for t in range(1, T + 1)}
+    pos = {t: var(f"posLoadGenerateMismatch[SingleBus,{t}]", 0.0, INF, d["LoadMismatchPenalty"])
+           for t in range(1, T + 1)}
+    neg = {t: var(f"negLoadGenerateMismatch[SingleBus,{t}]", 0.0, INF, d["LoadMismatchPenalty"])
+           for t in range(1, T + 1)}
+    rsf = {t: var(f"ReserveShortfall[{t}]", 0.0, INF, 1e5) for t in range(1, T + 1)}
+    demand, reserve = d["demand"], d["reserve"]
+    # system rows
+    row([(pos[t], 1.0) for t in range(1, T + 1)], 0.0, INF)
+    row([(neg[t], 1.0) for t in range(1, T + 1)], 0.0, INF)
+    for t in range(1, T + 1):
+        row([(ang[t], 1.0)], 0.0, 0.0)
+        terms = [(nd[t], 1.0), (lgm[t], 1.0)]
+        for g in gens:
+            terms += [(pg[g, t], 1.0), (on[g, t], par[g]["pmin"])]
+        row(terms, demand[t - 1], demand[t - 1])
+        row([(pos[t], 1.0), (neg[t], -1.0), (lgm[t], -1.0)], 0.0, 0.0)
+        row([(rsf[t], 1.0)], -INF, reserve[t - 1])
+        terms = [(nd[t], 1.0), (lgm[t], 1.0), (rsf[t], 1.0)]
+        for g in gens:
+            terms += [(mp[g, t], 1.0), (on[g, t], par[g]["pmin"])]
+        row(terms, demand[t - 1] + reserve[t - 1], INF)
+        row([(tpc[t], 1.0)] + [(pc[g, t], -1.0) for g in gens], 0.0, 0.0)
+        row([(tnl[t], 1.0)] + [(on[g, t], -par[g]["minprod"]) for g in gens], 0.0, 0.0)
+    for g in gens:
+        p = par[g]
+        span = p["pmax"] - p["pmin"]
+        for t in range(1, T + 1):
+            row([(pg[g, t], 1.0), (mp[g, t], -1.0)], -INF, 0.0)                      # PartB
+            last = t == T
+            if p["mut"] == 1:
+                row([(mp[g, t], 1.0), (on[g, t], -span), (st[g, t], p["pmax"] - p["sul"])], -INF, 0.0)
+                if last:
+                    row([(mp[g, t], 1.0), (on[g, t], -span)], -INF, 0.0)
+                else:
+                    row([(mp[g, t], 1.0), (on[g, t], -span), (sp_[g, t + 1], p["pmax"] - p["sdl"])], -INF, 0.0)
+            else:
+                terms = [(mp[g, t], 1.0), (on[g, t], -span), (st[g, t], p["pmax"] - p["sul"])]
+                if not last:
+                    terms.append((sp_[g, t + 1], p["pmax"] - p["sdl"]))
+                row(terms, -INF, 0.0)
+            if t == 1:                                                              # ramp up / down
+                row([(mp[g, 1], 1.0)], -INF, (p["pg0"] - p["pmin"]) * p["u0"] + p["rup"])
+                row([(pg[g, 1], -1.0)], -INF, p["rdn"] - (p["pg0"] - p["pmin"]) * p["u0"])
+            else:
+                row([(mp[g, t], 1.0), (pg[g, t - 1], -1.0)], -INF, p["rup"])
+                row([(pg[g, t - 1], 1.0), (pg[g, t], -1.0)], -INF, p["rdn"])
+            npc = len(p["pwp"]) - 1
+            row([(pp[g, t, i], 1.0) for i in range(npc)] + [(pg[g, t], -1.0)], 0.0, 0.0)
+            for i in range(npc):
+                row([(pp[g, t, i], 1.0), (on[g, t], -(p["pwp"][i + 1] - p["pwp"][i]))], -INF, 0.0)
+            if npc > 0:
+                terms = [(pc[g, t], 1.0)]
+                for i in range(npc):
+                    slope = (TPL * p["pwv"][i + 1] * p["fuel"] - TPL * p["pwv"][i] * p["fuel"]) \
+                        / (p["pwp"][i + 1] - p["pwp"][i])
+                    terms.append((pp[g, t, i], -slope))
+                row(terms, 0.0, 0.0)
+            # startup / shutdown matching and costs
+            row([(si[g, tp, tt], 1.0) for (tp, tt) in p["pairs"] if tt == t] + [(st[g, t], -1.0)], -INF, 0.0)
+            terms = [(suc[g, t], 1.0), (st[g, t], -p["scost"][-1])]
+            for s in range(1, len(p["lags"])):
+                coef = p["scost"][s - 1] - p["scost"][-1]
+                for tp in p["vstp"]:
+                    if p["lags"][s - 1] <= t - tp < p["lags"][s]:
+                        terms.append((si[g, tp, t], -coef))
+            row(terms, 0.0, 0.0)
+            row([(sdc[g, t], 1.0)], 0.0, 0.0)                                      # ShutdownFixedCost = 0
+            if t >= p["mu"]:
+                row([(st[g, i], 1.0) for i in range(max(1, t - p["mu"] + 1), t + 1)] + [(on[g, t], -1.0)],
+                    -INF, 0.0)
+            if t >= p["md"]:
+                row([(sp_[g, i], 1.0) for i in range(max(1, t - p["md"] + 1), t + 1)] + [(on[g, t], 1.0)],
+                    -INF, 1.0)
+            if t == 1:
+                row([(on[g, 1], 1.0), (st[g, 1], -1.0), (sp_[g, 1], 1.0)], p["u0"], p["u0"])
+            else:
+                row([(on[g, t], 1.0), (on[g, t - 1], -1.0), (st[g, t], -1.0), (sp_[g, t], 1.0)], 0.0, 0.0)
+        for tp in p["vstp"]:                                                        # ShutdownMatch
+            terms = [(si[g, a, b], 1.0) for (a, b) in p["pairs"] if a == tp]
+            if tp < 1:
+                if terms:
+                    row(terms, -INF, 1.0)
+            else:
+                row(terms + [(sp_[g, tp], -1.0)], -INF, 0.0)
+        if p["on_init"] > 0:
+            row([(on[g, t], 1.0) for t in range(1, T + 1) if t <= p["on_init"]], p["on_init"], p["on_init"])
+        if p["off_init"] > 0:
+            row([(on[g, t], 1.0) for t in range(1, T + 1) if t <= p["off_init"]], 0.0, 0.0)
+    n = len(lo)
+    A = sp.csr_matrix((rows_v, (rows_r, rows_c)), shape=(len(rl), n))
+    names = [None] * n
+    for k, j in cols.items():
+        names[j] = k
+    nonant = [on[g, t] for (g, t) in sorted(on)]     # sorted keys (scenario_tree.py:36)
+    return OScen(scenario_name, names, np.asarray(cost), A, np.asarray(rl), np.asarray(ru),
+                 np.asarray(lo), np.asarray(hi), [("ROOT", 1.0, nonant)])

@@ -176,3 +176,35 @@ def test_ctypes_structs_match_the_header_layout(tmp_path):
         assert got[(cname, "size")] == ctypes.sizeof(cls), cname
         for fname, _ in cls._fields_:
             assert got[(cname, fname)] == getattr(cls, fname).offset, (cname, fname)
+
+
+def test_uc_layout_matches_oracle():
+    """BASELINE config 4's model (examples/uc.py: ReferenceModel_OK.py's LP
+    relaxation on the WECC-240 data) against the oracle's independent
+    restatement (oracle/models.py uc): the same shape, nonants (UnitOn in
+    sorted key order) and, per scenario wind, the same LP optimum (HiGHS on
+    both); the batch carries each scenario's wind bounds."""
+    import scipy.sparse as sp
+    from mpisppy_amd.examples import uc
+    from oracle import models as om
+    from oracle.solve import _highs_solve
+    names = ["Scenario1", "Scenario7"]
+    bd = uc.batch_creator(names)
+    assert (bd.n, bd.m, bd.K) == (56869, 69902, 4080)
+    for s, nm in enumerate(names):
+        sc = om.uc(nm)
+        assert sc.A.shape == (bd.m, bd.n)
+        assert len(sc.nonant_idx) == bd.K
+        A = sp.csr_matrix((bd.vals[:, s], bd.col_idx, bd.row_ptr), shape=(bd.m, bd.n))
+        st1, x1, _, _ = _highs_solve(bd.c[:, s], None, A, bd.rl[:, s], bd.ru[:, s], bd.l[:, s], bd.u[:, s],
+                                     time_limit=120)
+        st2, x2, _, _ = _highs_solve(sc.c, None, sc.A, sc.rl, sc.ru, sc.l, sc.u, time_limit=120)
+        v1 = float(bd.c[:, s] @ x1 + bd.const[s])
+        v2 = float(sc.c @ x2)
+        assert abs(v1 - v2) <= 1e-9 * abs(v2), (nm, v1, v2)
+        # nonant values of two exact vertices need not agree (degenerate LP);
+        # the nonant names are UnitOn in sorted (generator, period) order
+    nn = [bd.var_names[j] for j in bd.nonant_cols]
+    assert nn[0] == "UnitOn[('BRIDGER_20_6333_C', 1)]" and nn[1] == "UnitOn[('BRIDGER_20_6333_C', 2)]"
+    rhos = dict(uc.scenario_rhos(None))
+    assert len(rhos) == bd.K and min(rhos.values()) >= 0.0

@@ -518,3 +518,37 @@ def test_bundled_hydro_multistage_matches_oracle():
     assert abs(tb - ot) < 1e-9 * abs(ot)
     assert abs(eobj - oe) < 1e-7 * abs(oe)
     assert abs(conv - oc) < 1e-6 * abs(oc)
+
+
+@pytest.mark.parametrize("by", ["name", "vardata"])
+def test_rho_setter_matches_oracle(by):
+    """phbase.py:556-588: rho_setter(scenario) -> [(var, rho)]; the var given
+    by nonant name (batched scenarios, no models) or by VarData of the
+    scenario's model; the PH trajectory with per-slot rho equals the
+    oracle's with the same rho."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    from cpu_batch import CPUBatch
+    names = [f"scen{i}" for i in range(6)]
+    rho_of = {"WHEAT0": 0.5, "CORN0": 2.0, "SUGAR_BEETS0": 1.5}
+
+    def setter(scen):
+        if by == "name":
+            return [(f"DevotedAcreage[{c}]", r) for c, r in rho_of.items()]
+        return [(scen.DevotedAcreage[c], r) for c, r in rho_of.items()]
+
+    opts = _opts(PHIterLimit=6, per_scenario_models=(by == "vardata"))
+    ph = PH(dict(opts), names, farmer.scenario_creator, rho_setter=setter)
+    ph.batch = CPUBatch(ph.batch_data)
+    conv, eobj, tb = ph.ph_main()
+    orc = OraclePH(dict(opts), [om.farmer(n) for n in names])
+    order = ph.nonant_names()
+    r = np.array([rho_of[nm.split("[")[1].rstrip("]")] for nm in order])
+    orc.Iter0()
+    orc.rho = [r.copy() for _ in names]
+    orc.iterk_loop()
+    oe = orc.Eobjective()
+    assert ph._PHIter == orc.iters
+    assert abs(eobj - oe) < 1e-8 * abs(oe)
+    W = ph.W.view(ph.K, ph.S_loc).numpy().T
+    assert np.allclose(W, np.array(orc.W), rtol=1e-8, atol=1e-8)
