@@ -334,6 +334,28 @@ typedef struct ph_loop_pass_args {
 } ph_loop_pass_args;
 int ph_loop_bind_pass(ph_batch_t b, const ph_loop_pass_args *args);
 int ph_loop_pass(ph_batch_t b);
+/*
+ * Up to `iters` passes of the bound loop in one call, same results as that
+ * many ph_loop_pass calls (up to the summation order of Compute_Xbar's sums
+ * and of conv).  With PHGPU_PERSIST=1 (opt-in: at F2 it measured no faster
+ * than the per-pass kernels), one rank and the one-wave cached warm solve: a
+ * persistent launch runs whole passes with two grid barriers each (Compute_Xbar
+ * broadcast + Update_W + conv, then the cached map / register polish of every
+ * scenario and the next sums) while the owned scenarios' data stay in LDS;
+ * a pass with a polish failure is finished by the tail and post-solve
+ * kernels queued behind it (up to four such rounds per call).  Otherwise
+ * `iters` ph_loop_pass calls.  The caller reads ph_loop_status for how far
+ * it got.  Replaces: iterk_loop's loop body (phbase.py:1498-1553) repeated.
+ */
+int ph_loop_run(ph_batch_t b, int32_t iters);
+/* 1 when ph_loop_run takes the persistent path for the bound pass, else 0. */
+int ph_loop_persistent(ph_batch_t b);
+/*
+ * While timing is on (ph_batch_set_timing): the persistent launches' HIP
+ * events, out[3] = {loop_kernel launches, their total ms, passes they ran
+ * since ph_loop_reset} (synchronises).
+ */
+int ph_loop_read_timing(ph_batch_t b, double *out /*host [3]*/);
 
 /*
  * Kernel timing of ph_pdhg_solve with HIP events recorded on the batch's

@@ -288,6 +288,10 @@ struct LoopCtl {
   int32_t iter;   // PH iteration of the current pass (1-based)
   int32_t limit;  // PHIterLimit
   int32_t pend;   // lagged conv (several ranks): iteration whose partials wait, or 0
+  int32_t tailp;  // loop_kernel ended inside a pass with a tail list (summary_kernel finishes it)
+  int32_t iter_end;  // loop_kernel runs the passes before this iteration (ph_loop_run)
+  int32_t lpasses;   // passes loop_kernel completed since ph_loop_reset
+  int32_t pad_;
   double thresh;  // convthresh
   unsigned long long acc[6];  // not optimal, solves, iters sum, iters max, polished, cached
 };
@@ -317,6 +321,7 @@ enum DevCheck : int32_t {
   CHK_WS_RANGE = 4,       // a block past the HBM polish workspace (v0 = block, v1 = slices)
   CHK_QUEUE_RANGE = 5,    // a queue ticket below the grid (v0 = index, v1 = grid)
   CHK_GATHER_RANGE = 6,   // a ph_gather index past its source (v0 = index, v1 = element)
+  CHK_BARRIER = 7,        // a loop_kernel grid barrier timed out (v0 = generation, v1 = block)
 };
 __device__ __forceinline__ void dev_fail(int32_t *err, int code, int v0, int v1) {
   if (err && atomicCAS(err, 0, code) == 0) {
@@ -1690,49 +1695,18 @@ __device__ __forceinline__ void wave_stage2(double *d1, const double *__restrict
   }
 }
 
-// One wave evaluates SPW consecutive scenarios: their entries and static
-// blocks are contiguous, so they stage in one round of coalesced loads.
-template <int WPB, int SPW>
-__global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int w = threadIdx.x / WAVE;
-  const int sw = (blockIdx.x * WPB + w) * SPW;
-  if (sw >= a.S || stopped(a.ctl)) return;  // wave-uniform; no block barriers
+// The cached map of one scenario on one wave: `ent` / `sb` its cache entry
+// and static block (LDS), `vs` / `P` its values and the pattern for the
+// clipped case's SpMV, `xsw` [WAVE] LDS scratch.  AS_HIT: accepted and
+// written out (XN: the clipped scaled column value of lane `lane`);
+// AS_NOENTRY: no valid entry or the prox term changed; AS_MOVED: the active
+// set moved, `sig` = the primal-dual active-set step from the map's point.
+enum AsResult : int { AS_HIT = 0, AS_NOENTRY = 1, AS_MOVED = 2 };
+__device__ __forceinline__ int as_eval(const SolveArgs &a, int s, int lane, const double *ent,
+                                       const double *sb, const double *vs, const Pattern &P,
+                                       double *xsw, int ok, double hk_l, double qk_l, double cst_l,
+                                       int kslot, double &XN_out, unsigned long long (&sig)[4]) {
   const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m);
-  const int SBW = 4 * n + 3 * m;
-  const int ns = (a.S - sw) < SPW ? (a.S - sw) : SPW;  // scenarios of this wave
-  double *ent0 = lds + (size_t)w * (SPW * (a.CW + SBW) + WAVE);
-  double *sb0 = ent0 + SPW * a.CW;
-  double *xsw = sb0 + SPW * SBW;  // [WAVE] scratch for the clipped case
-  // ---- everything of the wave's scenarios in one round of loads
-  int okv[SPW];
-  double hkv[SPW], qkv[SPW], cstv[SPW];
-#pragma unroll
-  for (int u = 0; u < SPW; ++u) {
-    const int s = sw + u;
-    okv[u] = u < ns ? a.cache_ok[s] : 0;
-    hkv[u] = qkv[u] = cstv[u] = 0.0;
-    if (u < ns && lane < K) {
-      const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
-      const double xb = a.xbar[(size_t)lane * S + s];
-      hkv[u] = a.w_on * W - a.prox_on * r * xb;
-      qkv[u] = a.prox_on * r;
-      cstv[u] = a.prox_on * 0.5 * r * xb * xb;
-    }
-  }
-  const int kslot = lane < n ? a.slot_of_col[lane] : -1;
-  wave_stage2(ent0, a.cache + (size_t)sw * a.CW, ns * a.CW, sb0, a.sb + (size_t)sw * SBW,
-              ns * SBW, lane);
-  wsync();
-#pragma unroll
-  for (int u = 0; u < SPW; ++u) {
-  if (u >= ns) break;
-  const int s = sw + u;
-  const int ok = okv[u];
-  const double hk_l = hkv[u], qk_l = qkv[u], cst_l = cstv[u];
-  const double *ent = ent0 + (size_t)u * a.CW;
-  const double *sb = sb0 + (size_t)u * SBW;
   const double *B = ent + K;
   double DC = 1.0, G = 0.0, L = 0.0, U = 0.0, XU = 0.0, ATY = 0.0;
   if (lane < n) {
@@ -1772,13 +1746,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   if (kslot >= 0) G += hj * DC;
   const double Q = (kslot >= 0 ? qj : 0.0) * DC * DC;
   // the entry must exist and belong to this prox term
-  if (!ok || __ballot(lane < n && kslot >= 0 && keyj != Q)) {
-    if (lane == 0) {
-      a.hint_ok[s] = 0;
-      list_push(a.wl, a.wl_count, s, S, a.err);
-    }
-    continue;
-  }
+  if (!ok || __ballot(lane < n && kslot >= 0 && keyj != Q)) return AS_NOENTRY;
   double XN = lane < n ? clampd(XU, L, U) : 0.0;
   const double YN = YU;
   double AXN = AX;
@@ -1787,7 +1755,7 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
     // a column left its bounds: the products of the clipped point by SpMV
     if (lane < n) xsw[lane] = XN;
     wsync();
-    AXN = pat_rowdot(lane, m, a.P, a.vals_s + (size_t)s * a.nnz, xsw);
+    AXN = pat_rowdot(lane, m, P, vs, xsw);
   }
   double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   double lam = 0.0;
@@ -1799,18 +1767,12 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   double ep, ed, eg, pobj, dobj;
   kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
   if (!(ep <= a.tol && ed <= a.tol && eg <= a.tol)) {
-    // the active set moved: hand pdhg_kernel the primal-dual active-set
-    // step from the map's (unclipped) point as the polish's first guess
+    // the active set moved: the primal-dual active-set step from the map's
+    // (unclipped) point, the polish's first guess
     const double lamu = Q * XU + G - ATY;
     const ActiveSet as = classify_pdas(lane, n, m, XU, lamu, YU, AX, L, U, RL, RU);
-    unsigned long long sig[4];
     as.signature(sig);
-    if (lane < 4) a.hint[4 * (size_t)s + lane] = sig[lane];
-    if (lane == 0) {
-      a.hint_ok[s] = 1;
-      list_push(a.wl, a.wl_count, s, S, a.err);
-    }
-    continue;
+    return AS_MOVED;
   }
   if (lane < n) a.x[(size_t)lane * S + s] = XN * DC;
   if (lane < m) a.y[(size_t)lane * S + s] = YN * DR;
@@ -1825,6 +1787,63 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
     dg[2] = eg;
     dg[3] = -1.0;
     dg[4] = 3.0;
+  }
+  XN_out = XN;
+  return AS_HIT;
+}
+
+// One wave evaluates SPW consecutive scenarios: their entries and static
+// blocks are contiguous, so they stage in one round of coalesced loads.
+template <int WPB, int SPW>
+__global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w = threadIdx.x / WAVE;
+  const int sw = (blockIdx.x * WPB + w) * SPW;
+  if (sw >= a.S || stopped(a.ctl)) return;  // wave-uniform; no block barriers
+  const int S = a.S, n = a.n, m = a.m, K = a.K;
+  const int SBW = 4 * n + 3 * m;
+  const int ns = (a.S - sw) < SPW ? (a.S - sw) : SPW;  // scenarios of this wave
+  double *ent0 = lds + (size_t)w * (SPW * (a.CW + SBW) + WAVE);
+  double *sb0 = ent0 + SPW * a.CW;
+  double *xsw = sb0 + SPW * SBW;  // [WAVE] scratch for the clipped case
+  // ---- everything of the wave's scenarios in one round of loads
+  int okv[SPW];
+  double hkv[SPW], qkv[SPW], cstv[SPW];
+#pragma unroll
+  for (int u = 0; u < SPW; ++u) {
+    const int s = sw + u;
+    okv[u] = u < ns ? a.cache_ok[s] : 0;
+    hkv[u] = qkv[u] = cstv[u] = 0.0;
+    if (u < ns && lane < K) {
+      const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
+      const double xb = a.xbar[(size_t)lane * S + s];
+      hkv[u] = a.w_on * W - a.prox_on * r * xb;
+      qkv[u] = a.prox_on * r;
+      cstv[u] = a.prox_on * 0.5 * r * xb * xb;
+    }
+  }
+  const int kslot = lane < n ? a.slot_of_col[lane] : -1;
+  wave_stage2(ent0, a.cache + (size_t)sw * a.CW, ns * a.CW, sb0, a.sb + (size_t)sw * SBW,
+              ns * SBW, lane);
+  wsync();
+#pragma unroll
+  for (int u = 0; u < SPW; ++u) {
+  if (u >= ns) break;
+  const int s = sw + u;
+  const int ok = okv[u];
+  const double hk_l = hkv[u], qk_l = qkv[u], cst_l = cstv[u];
+  const double *ent = ent0 + (size_t)u * a.CW;
+  const double *sb = sb0 + (size_t)u * SBW;
+  double XN = 0.0;
+  unsigned long long sig[4];
+  const int r = as_eval(a, s, lane, ent, sb, a.vals_s + (size_t)s * a.nnz, a.P, xsw, ok, hk_l, qk_l,
+                        cst_l, kslot, XN, sig);
+  if (r == AS_HIT) continue;
+  if (r == AS_MOVED && lane < 4) a.hint[4 * (size_t)s + lane] = sig[lane];
+  if (lane == 0) {
+    a.hint_ok[s] = r == AS_MOVED ? 1 : 0;
+    list_push(a.wl, a.wl_count, s, S, a.err);
   }
   }  // scenarios of the wave
 }
@@ -2009,6 +2028,308 @@ __device__ __forceinline__ unsigned long long abs_key(double v) {  // order of |
   return (unsigned long long)__double_as_longlong(fabs(v));
 }
 
+// One wave's LDS for polish_one: staging rows [RG_KST], solutions
+// [1+RG_K][WAVE], the current point xs / ys [WAVE] each, and the unknown
+// positions of columns / rows [WAVE] each.
+struct PolScratch {
+  double *kst, *sol, *xs, *ys;
+  int32_t *cpos, *rpos;
+};
+struct PatLds {  // the pattern in LDS (CSR row_ptr / col_idx, CSC col_ptr / row / CSR position)
+  const int32_t *rp, *ci, *cp, *cr, *ck;
+};
+
+// The register Gauss-Jordan polish of scenario s from the active set sig0
+// (see above): `vl` its scaled values, `sb` its static block, (hk_l, qk_l,
+// cst_l) lane k's PH terms of slot k.  Accepted: the outputs and the cache
+// entry (and its LDS copy ent2, when given) written, XN_out = the scaled
+// column value of lane `lane`, true.  Otherwise false (nothing written).
+__device__ __forceinline__ bool polish_one(const SolveArgs &a, int s, int lane, const PolScratch &w,
+                                           const PatLds &pt, const double *vl, const double *sb,
+                                           double hk_l, double qk_l, double cst_l, int kslot,
+                                           const unsigned long long (&sig0)[4], double *ent2,
+                                           double &XN_out) {
+  const int S = a.S, n = a.n, m = a.m, K = a.K;
+  double *kst = w.kst, *sol = w.sol, *xs = w.xs, *ys = w.ys;
+  int32_t *cpos = w.cpos, *rpos = w.rpos;
+  const int32_t *rp = pt.rp, *ci = pt.ci, *cp = pt.cp, *cr = pt.cr, *ck = pt.ck;
+  auto rowdot = [&]() {  // row `lane` of A xs
+    double acc = 0.0;
+    if (lane < m)
+      for (int p = rp[lane]; p < rp[lane + 1]; ++p) acc = fma(vl[p], xs[ci[p]], acc);
+    return acc;
+  };
+  auto coldot = [&]() {  // column `lane` of A' ys
+    double acc = 0.0;
+    if (lane < n)
+      for (int p = cp[lane]; p < cp[lane + 1]; ++p) acc = fma(vl[ck[p]], ys[cr[p]], acc);
+    return acc;
+  };
+  unsigned long long tq = a.prof ? wall_clock64() : 0ull;  // phase clock (debug)
+  auto tick = [&](int slot) {
+    if (a.prof) {
+      const unsigned long long t = wall_clock64();
+      if (lane == 0) atomicAdd(&a.prof[slot], t - tq);
+      tq = t;
+    }
+  };
+  // ---- scenario data (scaled): static block, PH terms
+  double G = 0.0, L = 0.0, U = 0.0, DC = 1.0, RL = 0.0, RU = 0.0, DR = 1.0;
+  if (lane < n) {
+    G = sb[lane];
+    L = sb[n + lane];
+    U = sb[2 * n + lane];
+    DC = sb[3 * n + lane];
+  }
+  if (lane < m) {
+    RL = sb[4 * n + lane];
+    RU = sb[4 * n + m + lane];
+    DR = sb[4 * n + 2 * m + lane];
+  }
+  const double HL = __shfl(hk_l, kslot >= 0 ? kslot : 0, WAVE) * (kslot >= 0 ? 1.0 : 0.0);
+  const double qj = __shfl(qk_l, kslot >= 0 ? kslot : 0, WAVE);
+  G += HL * DC;
+  const double Q = (kslot >= 0 ? qj : 0.0) * DC * DC;
+  const double cst = wave_sum(cst_l);
+  ActiveSet as = set_from_sig(lane, sig0);
+  unsigned long long prev[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  const bool done = K > RG_K;  // outside the register shape: straight to the tail
+  tick(10);  // scenario loads
+  for (int round = 0; round < POLISH_ROUNDS && !done; ++round) {
+    unsigned long long sig[4];
+    as.signature(sig);
+    if (same_sig(sig, prev)) break;  // cycle
+    for (int i = 0; i < 4; ++i) prev[i] = sig[i];
+    // ---- the active set's KKT system
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const bool fr = lane < n && as.cs == 0;
+    const bool ac = lane < m && as.rs != 0;
+    const unsigned long long fm = __ballot(fr), am = __ballot(ac);
+    const int nF = __popcll(fm), N = nF + __popcll(am);
+    if (N > RG_R0) break;
+    const int pF = __popcll(fm & below), pR = nF + __popcll(am & below);
+    const double xfix = as.cs == 1 ? L : (as.cs == 2 ? U : 0.0);
+    wsync();
+    if (lane < n) {
+      cpos[lane] = fr ? pF : -1;
+      xs[lane] = xfix;
+    }
+    if (lane < m) rpos[lane] = ac ? pR : -1;
+    for (int q = lane; q < N * RG_W; q += WAVE) kst[q] = 0.0;
+    for (int q = lane; q < (1 + K) * WAVE; q += WAVE) sol[q] = 0.0;
+    wsync();
+    if (fr) {  // stationarity row of free column `lane`
+      double *row = kst + pF * RG_W;
+      row[pF] = Q;
+      row[RG_R0] = -G;
+      if (kslot >= 0) row[RG_R0 + 1 + kslot] = -DC;
+      for (int p = cp[lane]; p < cp[lane + 1]; ++p) {
+        const int e = rpos[cr[p]];
+        if (e >= 0) row[e] = -vl[ck[p]];
+      }
+    }
+    if (ac) {  // active row `lane`
+      double *row = kst + pR * RG_W;
+      double rhs = as.rs == 1 ? RL : RU;
+      for (int p = rp[lane]; p < rp[lane + 1]; ++p) {
+        const int j = ci[p];
+        const int e = cpos[j];
+        if (e >= 0) row[e] = vl[p];
+        else rhs -= vl[p] * xs[j];
+      }
+      row[RG_R0] = rhs;
+    }
+    wsync();
+    double rg[RG_W];
+#pragma unroll
+    for (int c = 0; c < RG_W; ++c) rg[c] = lane < N ? kst[lane * RG_W + c] : 0.0;
+    tick(11);  // system build
+    // ---- Gauss-Jordan in registers
+    unsigned long long amax_k = 0ull;
+#pragma unroll
+    for (int c = 0; c < RG_R0; ++c) amax_k = umax64(amax_k, c < N ? abs_key(rg[c]) : 0ull);
+    const double amax = __longlong_as_double((long long)wave_max_key(amax_k));
+    const double piv_min = 1e-11 * (amax > 0.0 ? amax : 1.0);
+    bool used = false;
+    int myunk = -1;
+    double pivv = 1.0;
+#pragma unroll
+    for (int kk = 0; kk < RG_R0; ++kk) {
+      if (kk < N) {
+        const unsigned long long key =
+            (!used && lane < N) ? ((abs_key(rg[kk]) & ~63ull) | (unsigned long long)(63 - lane)) : 0ull;
+        const unsigned long long kmax = wave_max_key(key);
+        const double pabs = __longlong_as_double((long long)(kmax & ~63ull));
+        if (pabs > piv_min) {  // else: dependent column, its unknown stays 0
+          const int p = 63 - (int)(kmax & 63ull);
+          const double piv = readlane_f64(rg[kk], p);
+          const double inv = 1.0 / piv;
+          double prow[RG_W];
+#pragma unroll
+          for (int c = kk + 1; c < RG_W; ++c) prow[c] = readlane_f64(rg[c], p);
+          if (lane == p) {
+            used = true;
+            myunk = kk;
+            pivv = piv;
+          } else {
+            const double f = rg[kk] * inv;
+#pragma unroll
+            for (int c = kk + 1; c < RG_W; ++c) rg[c] = fma(-f, prow[c], rg[c]);
+            rg[kk] = 0.0;
+          }
+        }
+      }
+    }
+    tick(12);  // elimination
+    // unknowns to LDS: sol[t][unknown] for the current rhs (t = 0) and d/dh_k
+    if (used) {
+      const double ip = 1.0 / pivv;
+#pragma unroll
+      for (int t = 0; t <= RG_K; ++t)
+        if (t <= K) sol[t * WAVE + myunk] = rg[RG_R0 + t] * ip;
+    }
+    wsync();
+    const double XU = lane < n ? (fr ? sol[pF] : xfix) : 0.0;
+    const double YU = ac ? sol[pR] : 0.0;
+    // ---- KKT check of the clipped point
+    const double xn = lane < n ? clampd(XU, L, U) : 0.0;
+    const double yn = lane < m ? YU : 0.0;
+    wsync();
+    if (lane < n) xs[lane] = xn;
+    if (lane < m) ys[lane] = yn;
+    wsync();
+    const double axn = rowdot();
+    const double aty = coldot();
+    double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    double lam = 0.0;
+    if (lane < n) kkt_terms_col(xn, G, Q, L, U, DC, aty, lam, v);
+    if (lane < m) kkt_terms_row(axn, yn, RL, RU, DR, v);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = wave_sum(v[i]);
+    double ep, ed, eg, pobj, dobj;
+    kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
+    tick(13);  // solution + KKT check
+    if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
+      // ---- accepted: refresh the cache entry (affine map at this h)
+      if (a.cache) {
+        double *cs = a.cache + (size_t)s * a.CW;
+        auto put = [&](int off, double val) {
+          cs[off] = val;
+          if (ent2) ent2[off] = val;
+        };
+        const int VL = cache_vlen(n, m);
+        // the 1+K vectors (u at this h, then d u / d h_k) to LDS, their
+        // products with A and A' in one pass over the pattern
+        double *xk = kst, *yk = kst + (1 + RG_K) * WAVE;
+        wsync();
+#pragma unroll
+        for (int t = 0; t <= RG_K; ++t) {
+          if (t <= K) {
+            xk[t * WAVE + lane] = lane < n ? (t == 0 ? XU : (fr ? sol[t * WAVE + pF] : 0.0)) : 0.0;
+            yk[t * WAVE + lane] = lane < m ? (t == 0 ? YU : (ac ? sol[t * WAVE + pR] : 0.0)) : 0.0;
+          }
+        }
+        wsync();
+        double pax[1 + RG_K], paty[1 + RG_K];
+#pragma unroll
+        for (int t = 0; t <= RG_K; ++t) pax[t] = paty[t] = 0.0;
+        if (lane < m)
+          for (int p = rp[lane]; p < rp[lane + 1]; ++p) {
+            const int j = ci[p];
+            const double av = vl[p];
+#pragma unroll
+            for (int t = 0; t <= RG_K; ++t)
+              if (t <= K) pax[t] = fma(av, xk[t * WAVE + j], pax[t]);
+          }
+        if (lane < n)
+          for (int p = cp[lane]; p < cp[lane + 1]; ++p) {
+            const int i = cr[p];
+            const double av = vl[ck[p]];
+#pragma unroll
+            for (int t = 0; t <= RG_K; ++t)
+              if (t <= K) paty[t] = fma(av, yk[t * WAVE + i], paty[t]);
+          }
+        double bx = XU, by = YU, bax = pax[0], baty = paty[0];
+#pragma unroll
+        for (int t = 1; t <= RG_K; ++t) {
+          if (t <= K) {
+            const double hk = __shfl(hk_l, t - 1, WAVE);
+            const double dx = xk[t * WAVE + lane], dy = yk[t * WAVE + lane];
+            const int dk = K + t * VL;  // D_k's offset in the entry
+            if (lane < n) {
+              put(dk + cv_x(n, m) + lane, dx);
+              put(dk + cv_aty(n, m) + lane, paty[t]);
+            }
+            if (lane < m) {
+              put(dk + cv_y(n, m) + lane, dy);
+              put(dk + cv_ax(n, m) + lane, pax[t]);
+            }
+            bx -= hk * dx;
+            by -= hk * dy;
+            bax -= hk * pax[t];
+            baty -= hk * paty[t];
+          }
+        }
+        const int jk = lane < K ? a.nonant_col[lane] : 0;
+        const double dck = __shfl(DC, jk, WAVE);
+        const double key = qk_l;
+        if (lane < K) put(lane, key * dck * dck);  // scaled Q of slot `lane`'s column
+        if (lane < n) {
+          put(K + cv_x(n, m) + lane, bx);
+          put(K + cv_aty(n, m) + lane, baty);
+        }
+        if (lane < m) {
+          put(K + cv_y(n, m) + lane, by);
+          put(K + cv_ax(n, m) + lane, bax);
+        }
+        if (lane == 0) a.cache_ok[s] = 1;
+      }
+      tick(14);  // cache store
+      if (a.prof && lane == 0) atomicAdd(&a.prof[15], 1ull);
+      if (lane < n) a.x[(size_t)lane * S + s] = xn * DC;
+      if (lane < m) a.y[(size_t)lane * S + s] = yn * DR;
+      if (lane == 0) {
+        a.status[s] = PH_STATUS_OPTIMAL;
+        a.iters[s] = 0;
+        a.pobj[s] = pobj;
+        a.dbound[s] = dobj;
+        double *dg = a.diag + PH_DIAG_W * (size_t)s;
+        dg[0] = ep;
+        dg[1] = ed;
+        dg[2] = eg;
+        dg[3] = -1.0;
+        dg[4] = 1.0;
+      }
+      XN_out = xn;
+      return true;
+    }
+    // ---- primal-dual active-set step from the unclipped solution
+    const bool clipped = __ballot(lane < n && XU != xn) != 0ull;
+    double AXU = axn;
+    const double LAMU = lam + Q * (XU - xn);
+    wsync();
+    if (clipped) {
+      if (lane < n) xs[lane] = XU;
+      wsync();
+      AXU = rowdot();
+    }
+    as = classify_pdas(lane, n, m, XU, LAMU, yn, AXU, L, U, RL, RU);
+  }
+  return false;
+}
+
+// PH terms of slot `lane` (lane < K): h = w_on W - prox_on rho xbar, q =
+// prox_on rho, constant prox_on rho xbar^2 / 2.
+__device__ __forceinline__ void ph_lane_terms(const SolveArgs &a, int lane, double W, double r,
+                                              double xb, double &hk_l, double &qk_l, double &cst_l) {
+  hk_l = qk_l = cst_l = 0.0;
+  if (lane < a.K) {
+    hk_l = a.w_on * W - a.prox_on * r * xb;
+    qk_l = a.prox_on * r;
+    cst_l = a.prox_on * 0.5 * r * xb * xb;
+  }
+}
+
 __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
@@ -2035,285 +2356,28 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
     cr[q] = a.P.csc_row[q];
     ck[q] = a.P.csc_k[q];
   }
+  const PolScratch ws{kst, sol, xs, ys, cpos, rpos};
+  const PatLds pt{rp, ci, cp, cr, ck};
   const int kslot = lane < n ? a.slot_of_col[lane] : -1;
-  auto rowdot = [&]() {  // row `lane` of A xs
-    double acc = 0.0;
-    if (lane < m)
-      for (int p = rp[lane]; p < rp[lane + 1]; ++p) acc = fma(vl[p], xs[ci[p]], acc);
-    return acc;
-  };
-  auto coldot = [&]() {  // column `lane` of A' ys
-    double acc = 0.0;
-    if (lane < n)
-      for (int p = cp[lane]; p < cp[lane + 1]; ++p) acc = fma(vl[ck[p]], ys[cr[p]], acc);
-    return acc;
-  };
-  unsigned long long tq = a.prof ? wall_clock64() : 0ull;  // phase clock (debug)
-  auto tick = [&](int slot) {
-    if (a.prof) {
-      const unsigned long long t = wall_clock64();
-      if (lane == 0) atomicAdd(&a.prof[slot], t - tq);
-      tq = t;
-    }
-  };
   for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
     const int s = list_entry(a.wl, idx, S, a.err);
     if (s < 0) continue;  // (uniform: one wave)
     __syncthreads();  // LDS of the previous scenario
-    tick(9);  // pattern copy / previous scenario's tail
-    // ---- scenario data (scaled): static block, PH terms, values
-    const double *sb = a.sb + (size_t)s * (4 * n + 3 * m);
-    double G = 0.0, L = 0.0, U = 0.0, DC = 1.0, RL = 0.0, RU = 0.0, DR = 1.0;
-    if (lane < n) {
-      G = sb[lane];
-      L = sb[n + lane];
-      U = sb[2 * n + lane];
-      DC = sb[3 * n + lane];
-    }
-    if (lane < m) {
-      RL = sb[4 * n + lane];
-      RU = sb[4 * n + m + lane];
-      DR = sb[4 * n + 2 * m + lane];
-    }
-    double hk_l = 0.0, qk_l = 0.0, cst_l = 0.0;
-    if (lane < K) {
-      const double W = a.W[(size_t)lane * S + s], r = a.rho[(size_t)lane * S + s];
-      const double xb = a.xbar[(size_t)lane * S + s];
-      hk_l = a.w_on * W - a.prox_on * r * xb;
-      qk_l = a.prox_on * r;
-      cst_l = a.prox_on * 0.5 * r * xb * xb;
+    double hk_l, qk_l, cst_l;
+    {
+      const double W = lane < K ? a.W[(size_t)lane * S + s] : 0.0;
+      const double r = lane < K ? a.rho[(size_t)lane * S + s] : 0.0;
+      const double xb = lane < K ? a.xbar[(size_t)lane * S + s] : 0.0;
+      ph_lane_terms(a, lane, W, r, xb, hk_l, qk_l, cst_l);
     }
     unsigned long long sig0[4];
     for (int i = 0; i < 4; ++i) sig0[i] = a.hint[4 * (size_t)s + i];
     const double *vs = a.vals_s + (size_t)s * nnz;
     for (int q = lane; q < nnz; q += WAVE) vl[q] = vs[q];
-    const double HL = __shfl(hk_l, kslot >= 0 ? kslot : 0, WAVE) * (kslot >= 0 ? 1.0 : 0.0);
-    const double qj = __shfl(qk_l, kslot >= 0 ? kslot : 0, WAVE);
-    G += HL * DC;
-    const double Q = (kslot >= 0 ? qj : 0.0) * DC * DC;
-    const double cst = wave_sum(cst_l);
-    ActiveSet as = set_from_sig(lane, sig0);
-    unsigned long long prev[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-    bool done = K > RG_K;
-    tick(10);  // scenario loads  // outside the register shape: straight to pdhg_kernel
-    bool solved = false;
-    for (int round = 0; round < POLISH_ROUNDS && !done; ++round) {
-      unsigned long long sig[4];
-      as.signature(sig);
-      if (same_sig(sig, prev)) break;  // cycle
-      for (int i = 0; i < 4; ++i) prev[i] = sig[i];
-      // ---- the active set's KKT system
-      const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-      const bool fr = lane < n && as.cs == 0;
-      const bool ac = lane < m && as.rs != 0;
-      const unsigned long long fm = __ballot(fr), am = __ballot(ac);
-      const int nF = __popcll(fm), N = nF + __popcll(am);
-      if (N > RG_R0) break;
-      const int pF = __popcll(fm & below), pR = nF + __popcll(am & below);
-      const double xfix = as.cs == 1 ? L : (as.cs == 2 ? U : 0.0);
-      __syncthreads();
-      if (lane < n) {
-        cpos[lane] = fr ? pF : -1;
-        xs[lane] = xfix;
-      }
-      if (lane < m) rpos[lane] = ac ? pR : -1;
-      for (int q = lane; q < N * RG_W; q += WAVE) kst[q] = 0.0;
-      for (int q = lane; q < (1 + K) * WAVE; q += WAVE) sol[q] = 0.0;
-      __syncthreads();
-      if (fr) {  // stationarity row of free column `lane`
-        double *row = kst + pF * RG_W;
-        row[pF] = Q;
-        row[RG_R0] = -G;
-        if (kslot >= 0) row[RG_R0 + 1 + kslot] = -DC;
-        for (int p = cp[lane]; p < cp[lane + 1]; ++p) {
-          const int e = rpos[cr[p]];
-          if (e >= 0) row[e] = -vl[ck[p]];
-        }
-      }
-      if (ac) {  // active row `lane`
-        double *row = kst + pR * RG_W;
-        double rhs = as.rs == 1 ? RL : RU;
-        for (int p = rp[lane]; p < rp[lane + 1]; ++p) {
-          const int j = ci[p];
-          const int e = cpos[j];
-          if (e >= 0) row[e] = vl[p];
-          else rhs -= vl[p] * xs[j];
-        }
-        row[RG_R0] = rhs;
-      }
-      __syncthreads();
-      double rg[RG_W];
-#pragma unroll
-      for (int c = 0; c < RG_W; ++c) rg[c] = lane < N ? kst[lane * RG_W + c] : 0.0;
-      tick(11);  // system build
-      // ---- Gauss-Jordan in registers
-      unsigned long long amax_k = 0ull;
-#pragma unroll
-      for (int c = 0; c < RG_R0; ++c) amax_k = umax64(amax_k, c < N ? abs_key(rg[c]) : 0ull);
-      const double amax = __longlong_as_double((long long)wave_max_key(amax_k));
-      const double piv_min = 1e-11 * (amax > 0.0 ? amax : 1.0);
-      bool used = false;
-      int myunk = -1;
-      double pivv = 1.0;
-#pragma unroll
-      for (int kk = 0; kk < RG_R0; ++kk) {
-        if (kk < N) {
-          const unsigned long long key =
-              (!used && lane < N) ? ((abs_key(rg[kk]) & ~63ull) | (unsigned long long)(63 - lane)) : 0ull;
-          const unsigned long long kmax = wave_max_key(key);
-          const double pabs = __longlong_as_double((long long)(kmax & ~63ull));
-          if (pabs > piv_min) {  // else: dependent column, its unknown stays 0
-            const int p = 63 - (int)(kmax & 63ull);
-            const double piv = readlane_f64(rg[kk], p);
-            const double inv = 1.0 / piv;
-            double prow[RG_W];
-#pragma unroll
-            for (int c = kk + 1; c < RG_W; ++c) prow[c] = readlane_f64(rg[c], p);
-            if (lane == p) {
-              used = true;
-              myunk = kk;
-              pivv = piv;
-            } else {
-              const double f = rg[kk] * inv;
-#pragma unroll
-              for (int c = kk + 1; c < RG_W; ++c) rg[c] = fma(-f, prow[c], rg[c]);
-              rg[kk] = 0.0;
-            }
-          }
-        }
-      }
-      tick(12);  // elimination
-      // unknowns to LDS: sol[t][unknown] for the current rhs (t = 0) and d/dh_k
-      if (used) {
-        const double ip = 1.0 / pivv;
-#pragma unroll
-        for (int t = 0; t <= RG_K; ++t)
-          if (t <= K) sol[t * WAVE + myunk] = rg[RG_R0 + t] * ip;
-      }
-      __syncthreads();
-      const double XU = lane < n ? (fr ? sol[pF] : xfix) : 0.0;
-      const double YU = ac ? sol[pR] : 0.0;
-      // ---- KKT check of the clipped point
-      const double xn = lane < n ? clampd(XU, L, U) : 0.0;
-      const double yn = lane < m ? YU : 0.0;
-      __syncthreads();
-      if (lane < n) xs[lane] = xn;
-      if (lane < m) ys[lane] = yn;
-      __syncthreads();
-      const double axn = rowdot();
-      const double aty = coldot();
-      double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-      double lam = 0.0;
-      if (lane < n) kkt_terms_col(xn, G, Q, L, U, DC, aty, lam, v);
-      if (lane < m) kkt_terms_row(axn, yn, RL, RU, DR, v);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) v[i] = wave_sum(v[i]);
-      double ep, ed, eg, pobj, dobj;
-      kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
-      tick(13);  // solution + KKT check
-      if (ep <= a.tol && ed <= a.tol && eg <= a.tol) {
-        // ---- accepted: refresh the cache entry (affine map at this h)
-        if (a.cache) {
-          double *cs = a.cache + (size_t)s * a.CW;
-          const int VL = cache_vlen(n, m);
-          // the 1+K vectors (u at this h, then d u / d h_k) to LDS, their
-          // products with A and A' in one pass over the pattern
-          double *xk = kst, *yk = kst + (1 + RG_K) * WAVE;
-          __syncthreads();
-#pragma unroll
-          for (int t = 0; t <= RG_K; ++t) {
-            if (t <= K) {
-              xk[t * WAVE + lane] = lane < n ? (t == 0 ? XU : (fr ? sol[t * WAVE + pF] : 0.0)) : 0.0;
-              yk[t * WAVE + lane] = lane < m ? (t == 0 ? YU : (ac ? sol[t * WAVE + pR] : 0.0)) : 0.0;
-            }
-          }
-          __syncthreads();
-          double pax[1 + RG_K], paty[1 + RG_K];
-#pragma unroll
-          for (int t = 0; t <= RG_K; ++t) pax[t] = paty[t] = 0.0;
-          if (lane < m)
-            for (int p = rp[lane]; p < rp[lane + 1]; ++p) {
-              const int j = ci[p];
-              const double av = vl[p];
-#pragma unroll
-              for (int t = 0; t <= RG_K; ++t)
-                if (t <= K) pax[t] = fma(av, xk[t * WAVE + j], pax[t]);
-            }
-          if (lane < n)
-            for (int p = cp[lane]; p < cp[lane + 1]; ++p) {
-              const int i = cr[p];
-              const double av = vl[ck[p]];
-#pragma unroll
-              for (int t = 0; t <= RG_K; ++t)
-                if (t <= K) paty[t] = fma(av, yk[t * WAVE + i], paty[t]);
-            }
-          double bx = XU, by = YU, bax = pax[0], baty = paty[0];
-#pragma unroll
-          for (int t = 1; t <= RG_K; ++t) {
-            if (t <= K) {
-              const double hk = __shfl(hk_l, t - 1, WAVE);
-              const double dx = xk[t * WAVE + lane], dy = yk[t * WAVE + lane];
-              double *Dk = cs + K + (size_t)t * VL;
-              if (lane < n) {
-                Dk[cv_x(n, m) + lane] = dx;
-                Dk[cv_aty(n, m) + lane] = paty[t];
-              }
-              if (lane < m) {
-                Dk[cv_y(n, m) + lane] = dy;
-                Dk[cv_ax(n, m) + lane] = pax[t];
-              }
-              bx -= hk * dx;
-              by -= hk * dy;
-              bax -= hk * pax[t];
-              baty -= hk * paty[t];
-            }
-          }
-          double *B = cs + K;
-          const int jk = lane < K ? a.nonant_col[lane] : 0;
-          const double dck = __shfl(DC, jk, WAVE);
-          const double key = qk_l;
-          if (lane < K) cs[lane] = key * dck * dck;  // scaled Q of slot `lane`'s column
-          if (lane < n) {
-            B[cv_x(n, m) + lane] = bx;
-            B[cv_aty(n, m) + lane] = baty;
-          }
-          if (lane < m) {
-            B[cv_y(n, m) + lane] = by;
-            B[cv_ax(n, m) + lane] = bax;
-          }
-          if (lane == 0) a.cache_ok[s] = 1;
-        }
-        tick(14);  // cache store
-        if (a.prof && lane == 0) atomicAdd(&a.prof[15], 1ull);
-        if (lane < n) a.x[(size_t)lane * S + s] = xn * DC;
-        if (lane < m) a.y[(size_t)lane * S + s] = yn * DR;
-        if (lane == 0) {
-          a.status[s] = PH_STATUS_OPTIMAL;
-          a.iters[s] = 0;
-          a.pobj[s] = pobj;
-          a.dbound[s] = dobj;
-          double *dg = a.diag + PH_DIAG_W * (size_t)s;
-          dg[0] = ep;
-          dg[1] = ed;
-          dg[2] = eg;
-          dg[3] = -1.0;
-          dg[4] = 1.0;
-        }
-        solved = true;
-        break;
-      }
-      // ---- primal-dual active-set step from the unclipped solution
-      const bool clipped = __ballot(lane < n && XU != xn) != 0ull;
-      double AXU = axn;
-      const double LAMU = lam + Q * (XU - xn);
-      __syncthreads();
-      if (clipped) {
-        if (lane < n) xs[lane] = XU;
-        __syncthreads();
-        AXU = rowdot();
-      }
-      as = classify_pdas(lane, n, m, XU, LAMU, yn, AXU, L, U, RL, RU);
-    }
+    wsync();
+    double XN = 0.0;
+    const bool solved = polish_one(a, s, lane, ws, pt, vl, a.sb + (size_t)s * (4 * n + 3 * m), hk_l,
+                                   qk_l, cst_l, kslot, sig0, nullptr, XN);
     if (!solved && lane == 0) {  // tail_kernel: warm polish from the point, PDHG, rescue
       a.hint_ok[s] = 0;
       list_push(a.wl2, a.wl2_count, s, S, a.err);
@@ -2527,9 +2591,11 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
                                                        LoopCtl *ctl, XbarArgs xa,
                                                        const int32_t *__restrict__ ctr,
                                                        const int32_t *__restrict__ wl2,
-                                                       int32_t *err) {
+                                                       int32_t *err, int persist) {
   __shared__ unsigned long long red[5][MAX_WAVES];
   if (stopped(ctl)) return;
+  // after loop_kernel (ph_loop_run): only a pass it left with a tail list
+  if (persist && !*(volatile const int32_t *)&ctl->tailp) return;
   if (blockIdx.x > 0 && xa.C == 0) {  // device loop, one block per node slot
     xbar_sums_block(xa, blockIdx.x - 1);
     return;
@@ -2693,6 +2759,405 @@ __global__ void __launch_bounds__(POST_BLOCK) update_w_conv_kernel(
   }
 }
 
+// ------------------------------------------------------------------------
+// Persistent device loop (one rank, one-wave cached path; ph_loop_run).
+// One launch runs whole iterk_loop passes: the grid is exactly the blocks
+// that can be resident (one per CU: four waves at the polish's register
+// budget), every wave owns a fixed contiguous range of scenarios whose
+// cache entries, static blocks, values and PH terms stay in LDS across the
+// passes, and the passes' grid-wide steps are two barriers each:
+//   U: Compute_Xbar's broadcast + Update_W of the owned scenarios (LDS +
+//      the [K][S] outputs), the conv partial   -> barrier -> conv, stop test
+//   S: the cached map of every owned scenario, a miss polished at once by
+//      the same wave (polish_one), a polish failure pushed to the tail list;
+//      the owned scenarios' Compute_Xbar terms    -> barrier -> next sums
+// A pass with a tail list entry ends the launch (the host-queued tail_kernel
+// and summary_kernel finish that pass as in ph_pdhg_solve); the launch also
+// ends at ctl->iter_end, at convergence or at the iteration limit.  The
+// partials move through agent-scope atomic stores / loads and every block
+// combines them in block order, so all blocks hold the same sums and conv
+// (deterministic) and take the same decisions.  A barrier that waits past
+// LOOP_BAR_TICKS records CHK_BARRIER and aborts every block (no hang).
+// ------------------------------------------------------------------------
+constexpr int LOOP_WPB = 4;
+constexpr unsigned long long LOOP_BAR_TICKS = 400000000ull;  // wall clock (100 MHz): 4 s
+
+struct LoopArgs {
+  SolveArgs a;                 // the warm cached solve (a.wl2 / a.wl2_count: the tail list)
+  double *sums;                // [2G] Compute_Xbar sums of the current x (read at entry, written at a chunk end)
+  int G;
+  const int32_t *gid;          // [K][S]
+  const double *rho, *wc, *pc; // [K][S] (wc may be null)
+  double *xbar, *xsqbar, *W, *absdiff;
+  const double *wconv;         // [S]
+  double *hist;                // conv history
+  LoopCtl *ctl;
+  int32_t *ctr;                // the batch's counters (0: misses, 1, 2: tail list count, 6)
+  double *part_x;              // [grid][2G+2] sums / misses / tails partials
+  double *part_c;              // [grid] conv partials
+  int32_t *bar;                // [2] arrival counter, abort flag (zeroed before each launch)
+  int spw;                     // scenario slots per wave
+  unsigned long long *prof;    // phase clocks (ph_debug_prof slots 20-28) or null
+};
+
+// LDS carve of loop_kernel (doubles), shared by the host: pattern ints,
+// block scratch, then per wave: polish scratch, sums accumulators, the
+// resident arrays, ints.
+struct LoopLds {
+  int pat, blk, wave, total;   // sizes in doubles
+  // per-wave offsets (doubles) inside a wave's slice
+  int o_kst, o_sol, o_xs, o_ys, o_acc, o_ent, o_sb, o_vl, o_rho, o_w, o_pc, o_wc, o_xb, o_xn,
+      o_wcv, o_int;
+};
+__host__ __device__ inline LoopLds loop_lds(int n, int m, int nnz, int K, int G, int CW, int spw) {
+  LoopLds L{};
+  const int pat_ints = (m + 1) + (n + 1) + 3 * nnz;
+  L.pat = (pat_ints + 1) / 2;
+  L.blk = 256 + (2 * G + 2) + 8;  // combine scratch, sums + counts, flags
+  int o = 0;
+  L.o_kst = o; o += RG_KST;
+  L.o_sol = o; o += (1 + RG_K) * WAVE;
+  L.o_xs = o; o += WAVE;
+  L.o_ys = o; o += WAVE;
+  L.o_acc = o; o += 2 * G + 2;
+  L.o_ent = o; o += spw * CW;
+  L.o_sb = o; o += spw * (4 * n + 3 * m);
+  L.o_vl = o; o += spw * nnz;
+  L.o_rho = o; o += spw * K;
+  L.o_w = o; o += spw * K;
+  L.o_pc = o; o += spw * K;
+  L.o_wc = o; o += spw * K;
+  L.o_xb = o; o += spw * K;
+  L.o_xn = o; o += spw * K;
+  L.o_wcv = o; o += spw;
+  L.o_int = o; o += (2 * WAVE + spw * (K + 1) + 1) / 2;  // cpos, rpos, gid [spw][K], ok [spw]
+  L.wave = o;
+  L.total = L.pat + L.blk + LOOP_WPB * L.wave;
+  return L;
+}
+
+// Deterministic grid combine: out[q] = sum over blocks b in order of
+// part[b * PQ + q], q < Q (256 threads: 8 values x 32 ordered chunks per
+// pass; every block computes the same values).
+__device__ __forceinline__ void grid_combine(const double *part, int PQ, int Q, double *scr, double *out) {
+  const int NB = gridDim.x, per = (NB + 31) / 32;
+  for (int qb = 0; qb < Q; qb += 8) {
+    const int q = qb + (int)threadIdx.x / 32, c = (int)threadIdx.x % 32;
+    double t = 0.0;
+    if (q < Q) {
+      const int b1 = min(NB, (c + 1) * per);
+      for (int b0 = c * per; b0 < b1; b0 += 8) {  // eight loads in flight, then the adds in order
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = b0 + u < b1 ? sub(part + (size_t)(b0 + u) * PQ + q) : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t += v[u];
+      }
+    }
+    scr[threadIdx.x] = t;
+    __syncthreads();
+    if (threadIdx.x < 8 && qb + (int)threadIdx.x < Q) {
+      double u = 0.0;
+      for (int cc = 0; cc < 32; ++cc) u += scr[threadIdx.x * 32 + cc];
+      out[qb + threadIdx.x] = u;
+    }
+    __syncthreads();
+  }
+}
+
+// Grid barrier over a resident grid: wave 0's publishing stores are
+// complete before its arrival (vmcnt), then thread 0 waits for every
+// block's arrival of this generation.  False on an abort (timeout here or
+// in another block).
+__device__ __forceinline__ bool grid_sync(int32_t *bar, unsigned &gen, int *flag, int32_t *err) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    gen += 1u;
+    const int target = (int)(gen * gridDim.x);
+    __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        ok = 0;
+        break;
+      }
+      if (wall_clock64() - t0 > LOOP_BAR_TICKS) {
+        __hip_atomic_store(bar + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dev_fail(err, CHK_BARRIER, (int)gen, (int)blockIdx.x);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    *flag = ok;
+  }
+  __syncthreads();
+  return *(volatile int *)flag != 0;
+}
+
+__global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const SolveArgs &a = L.a;
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const int S = a.S, n = a.n, m = a.m, nnz = a.nnz, K = a.K, G = L.G, CW = a.CW;
+  const int SBW = 4 * n + 3 * m, PQ = 2 * G + 2;
+  LoopCtl *ctl = L.ctl;
+  const int stop0 = *(volatile int32_t *)&ctl->stop;
+  int it = *(volatile int32_t *)&ctl->iter;
+  const int iend = ctl->iter_end, limit = ctl->limit;
+  const double thresh = ctl->thresh;
+  const LoopLds lay = loop_lds(n, m, nnz, K, G, CW, L.spw);
+  // ---- LDS carve
+  int32_t *rp = (int32_t *)lds, *ci = rp + (m + 1), *cp = ci + nnz, *cr = cp + (n + 1), *ck = cr + nnz;
+  double *blk = lds + lay.pat;
+  double *scr = blk;                 // [256] combine scratch
+  double *sums_l = blk + 256;        // [2G] sums, [2G] misses, [2G+1] tails
+  int *flag = (int *)(sums_l + PQ);  // barrier result
+  double *wv = lds + lay.pat + lay.blk + (size_t)w * lay.wave;
+  double *ENT = wv + lay.o_ent, *SBV = wv + lay.o_sb, *VLV = wv + lay.o_vl;
+  double *RHO = wv + lay.o_rho, *WW = wv + lay.o_w, *PCV = wv + lay.o_pc, *WCV = wv + lay.o_wc;
+  double *XBV = wv + lay.o_xb, *XNV = wv + lay.o_xn, *WCONV = wv + lay.o_wcv, *ACC = wv + lay.o_acc;
+  int32_t *ints = (int32_t *)(wv + lay.o_int);
+  int32_t *cpos = ints, *rpos = ints + WAVE, *GID = ints + 2 * WAVE, *OKV = GID + L.spw * K;
+  const PolScratch ws{wv + lay.o_kst, wv + lay.o_sol, wv + lay.o_xs, wv + lay.o_ys, cpos, rpos};
+  const PatLds pt{rp, ci, cp, cr, ck};
+  const Pattern Pl{rp, ci, cp, cr, ck};
+  // ---- the wave's scenarios: [s0, s0 + ns)
+  const int NW = gridDim.x * LOOP_WPB, gw = blockIdx.x * LOOP_WPB + w;
+  const int q0 = S / NW, r0 = S % NW;
+  const int ns = q0 + (gw < r0 ? 1 : 0), s0 = gw * q0 + min(gw, r0);
+  // the largest range (uniform): a range past the slots is a host sizing error
+  const bool fits = q0 + (r0 > 0 ? 1 : 0) <= L.spw;
+  const bool ran = fits && stop0 == 0 && it < iend;
+  int stop = stop0, tail = 0, passes = 0;
+  unsigned long long n_pol = 0, n_hit = 0;
+  if (ran) {
+    // ---- resident data (once per launch)
+    for (int q = threadIdx.x; q <= m; q += blockDim.x) rp[q] = a.P.row_ptr[q];
+    for (int q = threadIdx.x; q <= n; q += blockDim.x) cp[q] = a.P.col_ptr[q];
+    for (int q = threadIdx.x; q < nnz; q += blockDim.x) {
+      ci[q] = a.P.col_idx[q];
+      cr[q] = a.P.csc_row[q];
+      ck[q] = a.P.csc_k[q];
+    }
+    for (int q = threadIdx.x; q < 2 * G; q += blockDim.x) sums_l[q] = L.sums[q];
+    wave_stage2(ENT, a.cache + (size_t)s0 * CW, ns * CW, SBV, a.sb + (size_t)s0 * SBW, ns * SBW, lane);
+    wave_stage2(VLV, a.vals_s + (size_t)s0 * nnz, ns * nnz, VLV, a.vals_s + (size_t)s0 * nnz, 0, lane);
+    for (int j = 0; j < ns; ++j) {
+      const int s = s0 + j;
+      if (lane < K) {
+        const size_t o = (size_t)lane * S + s;
+        RHO[j * K + lane] = L.rho[o];
+        WW[j * K + lane] = L.W[o];
+        PCV[j * K + lane] = L.pc[o];
+        WCV[j * K + lane] = L.wc ? L.wc[o] : 1.0;
+        XNV[j * K + lane] = a.x[(size_t)a.nonant_col[lane] * S + s];
+        GID[j * K + lane] = L.gid[o];
+      }
+      if (lane == 0) {
+        WCONV[j] = L.wconv[s];
+        OKV[j] = a.cache_ok[s];
+      }
+    }
+  }
+  const int kslot = lane < n ? a.slot_of_col[lane] : -1;
+  const int jk = lane < K ? a.nonant_col[lane] : 0;
+  unsigned gen = 0;
+  bool ok = ran, aborted = false;
+  // phase clocks (debug, thread 0 of each block): U, barrier U, combines,
+  // S, barrier S; per wave the polish time
+  unsigned long long tq = L.prof ? wall_clock64() : 0ull, tph[5] = {0, 0, 0, 0, 0}, tpol = 0, npolw = 0;
+  auto tick = [&](int i) {
+    if (L.prof) {
+      const unsigned long long t = wall_clock64();
+      tph[i] += t - tq;
+      tq = t;
+    }
+  };
+  __syncthreads();
+  if (!fits && threadIdx.x == 0 && blockIdx.x == 0) dev_fail(a.err, CHK_WS_RANGE, q0 + 1, L.spw);
+  while (ok) {
+    // ================= U: Compute_Xbar broadcast, Update_W, conv partial
+    double convw = 0.0;
+    for (int j = 0; j < ns; ++j) {
+      const int s = s0 + j;
+      double ad = 0.0;
+      if (lane < K) {
+        const size_t o = (size_t)lane * S + s;
+        const int g = GID[j * K + lane];
+        const double xb = sums_l[g], xsq = sums_l[G + g];
+        L.xbar[o] = xb;
+        L.xsqbar[o] = xsq;
+        XBV[j * K + lane] = xb;
+        const double d = XNV[j * K + lane] - xb;
+        double wn = WW[j * K + lane] + RHO[j * K + lane] * d;
+        if (L.wc) wn *= WCV[j * K + lane];
+        WW[j * K + lane] = wn;
+        L.W[o] = wn;
+        ad = fabs(d);
+      }
+      ad = wave_sum(ad);
+      if (lane == 0) L.absdiff[s] = ad;
+      convw += ad * WCONV[j];
+    }
+    if (lane == 0) scr[w] = convw;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int q = 0; q < LOOP_WPB; ++q) t += scr[q];
+      pub(L.part_c + blockIdx.x, t);
+      tick(0);
+      if (blockIdx.x == 0) {  // the pass's work-list counters (before any push: barrier)
+        __hip_atomic_store(L.ctr + 0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(L.ctr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(L.ctr + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(L.ctr + 6, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (!grid_sync(L.bar, gen, flag, a.err)) {
+      aborted = true;
+      break;
+    }
+    tick(1);
+    grid_combine(L.part_c, 1, 1, scr, sums_l + 2 * G);
+    tick(2);
+    const double conv = sums_l[2 * G];
+    if (threadIdx.x == 0 && blockIdx.x == 0) L.hist[it - 1] = conv;
+    if (conv < thresh) {
+      stop = 1;
+      break;
+    }
+    // ================= S: the solve of the owned scenarios
+    for (int q = lane; q < 2 * G; q += WAVE) ACC[q] = 0.0;
+    int nmiss = 0, ntail = 0, npol = 0;
+    wsync();
+    for (int j = 0; j < ns; ++j) {
+      const int s = s0 + j;
+      double hk_l, qk_l, cst_l;
+      ph_lane_terms(a, lane, lane < K ? WW[j * K + lane] : 0.0, lane < K ? RHO[j * K + lane] : 0.0,
+                    lane < K ? XBV[j * K + lane] : 0.0, hk_l, qk_l, cst_l);
+      const double *ent_j = ENT + (size_t)j * CW, *sb_j = SBV + (size_t)j * SBW, *vl_j = VLV + (size_t)j * nnz;
+      double XN = 0.0;
+      unsigned long long sig[4];
+      const int r = as_eval(a, s, lane, ent_j, sb_j, vl_j, Pl, ws.xs, OKV[j], hk_l, qk_l, cst_l, kslot,
+                            XN, sig);
+      bool solved = r == AS_HIT;
+      if (!solved) {
+        ++nmiss;
+        if (r == AS_MOVED) {
+          if (lane < 4) a.hint[4 * (size_t)s + lane] = sig[lane];
+          if (lane == 0) a.hint_ok[s] = 1;
+        } else {
+          for (int i = 0; i < 4; ++i) sig[i] = a.hint[4 * (size_t)s + i];
+        }
+        wsync();
+        const unsigned long long tp0 = L.prof ? wall_clock64() : 0ull;
+        solved = polish_one(a, s, lane, ws, pt, vl_j, sb_j, hk_l, qk_l, cst_l, kslot, sig,
+                            ENT + (size_t)j * CW, XN);
+        if (L.prof) {
+          tpol += wall_clock64() - tp0;
+          ++npolw;
+        }
+        if (solved) {
+          ++npol;
+          if (lane == 0) OKV[j] = 1;
+        } else {
+          ++ntail;
+          if (lane == 0) {
+            a.hint_ok[s] = 0;
+            list_push(a.wl2, a.wl2_count, s, S, a.err);
+          }
+        }
+      }
+      if (solved) {
+        // this scenario's nonant values and Compute_Xbar terms
+        const double dcj = __shfl(lane < n ? sb_j[3 * n + lane] : 1.0, jk, WAVE);
+        const double xj = __shfl(XN, jk, WAVE) * dcj;
+        if (lane < K) {
+          XNV[j * K + lane] = xj;
+          const int g = GID[j * K + lane];
+          const double p = PCV[j * K + lane];
+          ACC[g] += p * xj;
+          ACC[G + g] += p * xj * xj;
+        }
+      }
+      wsync();
+    }
+    if (lane == 0) {
+      ACC[2 * G] = (double)nmiss;
+      ACC[2 * G + 1] = (double)ntail;
+    }
+    __syncthreads();
+    tick(3);
+    // block partial (waves in order), published by wave 0
+    if (w == 0)
+      for (int q = lane; q < PQ; q += WAVE) {
+        double t = 0.0;
+        for (int ww = 0; ww < LOOP_WPB; ++ww) t += lds[lay.pat + lay.blk + (size_t)ww * lay.wave + lay.o_acc + q];
+        pub(L.part_x + (size_t)blockIdx.x * PQ + q, t);
+      }
+    if (!grid_sync(L.bar, gen, flag, a.err)) {
+      aborted = true;
+      break;
+    }
+    tick(4);
+    grid_combine(L.part_x, PQ, PQ, scr, sums_l);
+    tick(2);
+    n_pol += (unsigned long long)npol;
+    n_hit += (unsigned long long)(ns - nmiss);
+    if (sums_l[2 * G + 1] > 0.0) {  // a tail: the host-queued kernels finish this pass
+      tail = 1;
+      if (threadIdx.x == 0 && blockIdx.x == 0)
+        __hip_atomic_store(L.ctr + 0, (int)sums_l[2 * G], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      n_pol -= (unsigned long long)npol;  // (summary_kernel counts this pass)
+      n_hit -= (unsigned long long)(ns - nmiss);
+      break;
+    }
+    ++passes;
+    if (it >= limit) {
+      stop = 2;
+      break;
+    }
+    ++it;
+    if (it >= iend) break;  // chunk end
+  }
+  // ---- exit: the sums of the current x (the next launch starts from them),
+  // counters, then block 0 the loop state
+  if (ran && !aborted && !tail && blockIdx.x == 0)
+    for (int q = threadIdx.x; q < 2 * G; q += blockDim.x) L.sums[q] = sums_l[q];
+  if (lane == 0 && (n_pol | n_hit)) {
+    atomicAdd(&ctl->acc[4], n_pol);
+    atomicAdd(&ctl->acc[5], n_hit);
+  }
+  if (L.prof) {
+    if (threadIdx.x == 0) {
+      for (int i = 0; i < 5; ++i) atomicAdd(&L.prof[20 + i], tph[i]);
+      atomicMax(&L.prof[26], tph[3]);
+      if (blockIdx.x == 0) atomicAdd(&L.prof[25], (unsigned long long)passes);
+    }
+    if (lane == 0 && npolw) {
+      atomicAdd(&L.prof[27], tpol);
+      atomicAdd(&L.prof[28], npolw);
+    }
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    if (aborted) {  // (PH_EDEV at the next synchronising call) the queued kernels stand down
+      ctl->stop = 2;
+      ctl->tailp = 0;
+    } else if (ran) {
+      ctl->iter = it;
+      if (stop) ctl->stop = stop;
+      ctl->acc[1] += (unsigned long long)passes * (unsigned long long)S;
+      ctl->lpasses += passes;
+      ctl->tailp = tail;
+    } else {
+      ctl->tailp = 0;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) eval_obj_kernel(
     int S, int n, const double *__restrict__ c, const int32_t *__restrict__ slot_of_col,
     const double *__restrict__ x, const double *__restrict__ W,
@@ -2790,6 +3255,11 @@ struct ph_batch {
   size_t big_lds_bytes = 0;     // LDS of big_kernel (y + scratch)
   bool big_ylds = true;         // big_kernel<true>: y in LDS; <false>: y in the slice (m > ~20,000)
   int big_grid = 0;             // resident blocks of the big phase kernels
+  // persistent device loop (ph_loop_run, loop_kernel)
+  int loop_grid = 0, loop_spw = 0, loop_G = 0;  // resident blocks, scenario slots per wave, for G
+  size_t loop_lds_bytes = 0;
+  double *d_lpart = nullptr;    // [grid][2G+2] + [grid] partials
+  int32_t *d_lbar = nullptr;    // [2] barrier counter, abort flag
 };
 
 namespace {
@@ -2961,10 +3431,11 @@ static int check_dev(const int32_t (&e)[4]) {
   static const char *what[] = {"?", "work list pushed past its capacity S",
                                "work-list count above S", "work-list entry outside [0, S)",
                                "block past the HBM polish workspace", "work-queue ticket out of range",
-                               "gather index past its source array"};
+                               "gather index past its source array",
+                               "persistent-loop grid barrier timed out"};
   char msg[256];
   std::snprintf(msg, sizeof(msg), "device-side check failed: %s (code %d, values %d %d)",
-                what[(e[0] >= 1 && e[0] <= 6) ? e[0] : 0], e[0], e[1], e[2]);
+                what[(e[0] >= 1 && e[0] <= 7) ? e[0] : 0], e[0], e[1], e[2]);
   return fail(PH_EDEV, msg);
 }
 
@@ -3687,7 +4158,7 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   const int post_g = (b->loop_on && b->loop_xa.x == a.x) ? b->loop_xa.G * std::max(1, b->loop_xa.C) : 0;
   hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, a.status,
                      a.iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa,
-                     (const int32_t *)nullptr, (const int32_t *)nullptr, b->d_err);
+                     (const int32_t *)nullptr, (const int32_t *)nullptr, b->d_err, 0);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -3738,17 +4209,11 @@ static int cold_tail(ph_batch *b, SolveArgs &a, size_t lds) {
   return PH_OK;
 }
 
-extern "C" {
-
-int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double *xbar,
-                  double w_on, double prox_on, double *x, double *y, double *omega,
-                  int32_t *status, int32_t *iters, double *pobj, double *dbound,
-                  const ph_solve_opts *opts) {
-  if (!b || !b->bound) return fail(PH_EINVAL, "ph_pdhg_solve: batch not bound");
-  if (!x || (b->m && !y) || !omega || !status || !iters || !pobj || !dbound)
-    return fail(PH_EINVAL, "ph_pdhg_solve: null output");
-  if (b->K && (!W || !rho || !xbar)) return fail(PH_EINVAL, "ph_pdhg_solve: null W/rho/xbar");
-  SolveArgs a;
+// SolveArgs of one ph_pdhg_solve call (also the solve of a ph_loop_run launch).
+static void fill_solve_args(ph_batch *b, const double *W, const double *rho, const double *xbar,
+                            double w_on, double prox_on, double *x, double *y, double *omega,
+                            int32_t *status, int32_t *iters, double *pobj, double *dbound,
+                            const ph_solve_opts *opts, SolveArgs &a) {
   a.S = b->S; a.n = b->n; a.m = b->m; a.nnz = b->nnz;
   {  // PHGPU_OMEGA_SPAN: measurement hook (F3's degenerate LPs stall at 1e2)
     static const double span = [] {
@@ -3796,19 +4261,63 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   a.ctl = loop_ctl(b);
   a.prof = b->d_prof;
   a.err = b->d_err;
+}
+
+// The resident grid of pdhg_kernel (first use).
+static int ensure_pdhg_grid(ph_batch *b, size_t lds) {
+  if (b->pdhg_grid != 0) return PH_OK;
+  int per_cu = 0, cus = 0, dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  DISPATCH_EXT(64, 1, b->ext, {
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pdhg_kernel<B_, P_, E_>, B_, lds));
+  });
+  b->pdhg_grid = std::max(1, per_cu) * std::max(1, cus);
+  return PH_OK;
+}
+
+// tail_kernel over the tail list wl2 (the cached solve's misses the register
+// polish left): a small grid, its blocks exit at once when the list is empty.
+static int launch_tail(ph_batch *b, const SolveArgs &a, size_t lds) {
+  const int has_md = one_wave_rescue(b) ? 1 : 0;
+  if (has_md)
+    if (int rc = mid_init(b)) return rc;
+  size_t tlds = lds;
+  if (has_md) tlds = std::max(tlds, b->mid_plds_bytes);
+  DISPATCH_EXT(64, 1, b->ext, {
+    if (!b->miss_attr && tlds > 64 * 1024) {
+      HIP_OK(hipFuncSetAttribute((const void *)tail_kernel<E_>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)tlds));
+      b->miss_attr = true;
+    }
+    static const int tail_grid = [] {  // PHGPU_TAIL_GRID: measurement hook
+      const char *e = std::getenv("PHGPU_TAIL_GRID");
+      return e ? std::min(TAIL_GRID, std::max(1, std::atoi(e))) : 64;
+    }();
+    hipLaunchKernelGGL((tail_kernel<E_>), dim3(std::min(b->S, std::min(b->pdhg_grid, tail_grid))),
+                       dim3(WAVE), tlds, b->stream, a, b->md, has_md);
+  });
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
+extern "C" {
+
+int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double *xbar,
+                  double w_on, double prox_on, double *x, double *y, double *omega,
+                  int32_t *status, int32_t *iters, double *pobj, double *dbound,
+                  const ph_solve_opts *opts) {
+  if (!b || !b->bound) return fail(PH_EINVAL, "ph_pdhg_solve: batch not bound");
+  if (!x || (b->m && !y) || !omega || !status || !iters || !pobj || !dbound)
+    return fail(PH_EINVAL, "ph_pdhg_solve: null output");
+  if (b->K && (!W || !rho || !xbar)) return fail(PH_EINVAL, "ph_pdhg_solve: null W/rho/xbar");
+  SolveArgs a;
+  fill_solve_args(b, W, rho, xbar, w_on, prox_on, x, y, omega, status, iters, pobj, dbound, opts, a);
   if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_pdhg_solve: bad options");
   if (b->mid) return mid_solve(b, a, opts);
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
-  if (b->pdhg_grid == 0) {
-    int per_cu = 0, cus = 0, dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    DISPATCH_EXT(64, 1, b->ext, {
-      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pdhg_kernel<B_, P_, E_>, B_, lds));
-    });
-    b->pdhg_grid = std::max(1, per_cu) * std::max(1, cus);
-  }
+  if (int rc = ensure_pdhg_grid(b, lds)) return rc;
   // (in the device loop the convergence kernel has cleared the counters)
   if (!b->loop_on) {
     HIP_OK(hipMemsetAsync(b->d_ctr, 0, 3 * sizeof(int32_t), b->stream));
@@ -3866,26 +4375,8 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     hipLaunchKernelGGL(polish_kernel, dim3(std::min(b->S, POLISH_GRID)), dim3(WAVE),
                        polish_lds_bytes(b), b->stream, a);
     HIP_OK(hipGetLastError());
-    const int has_md = one_wave_rescue(b) ? 1 : 0;
-    if (has_md)
-      if (int rc = mid_init(b)) return rc;
-    size_t tlds = lds;
-    if (has_md) tlds = std::max(tlds, b->mid_plds_bytes);
     a.ul = nullptr;  // (the tail bounds its failures itself)
-    DISPATCH_EXT(64, 1, b->ext, {
-      if (!b->miss_attr && tlds > 64 * 1024) {
-        HIP_OK(hipFuncSetAttribute((const void *)tail_kernel<E_>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)tlds));
-        b->miss_attr = true;
-      }
-      static const int tail_grid = [] {  // PHGPU_TAIL_GRID: measurement hook
-        const char *e = std::getenv("PHGPU_TAIL_GRID");
-        return e ? std::min(TAIL_GRID, std::max(1, std::atoi(e))) : 64;
-      }();
-      hipLaunchKernelGGL((tail_kernel<E_>), dim3(std::min(b->S, std::min(b->pdhg_grid, tail_grid))),
-                         dim3(WAVE), tlds, b->stream, a, b->md, has_md);
-    });
-    HIP_OK(hipGetLastError());
+    if (int rc = launch_tail(b, a, lds)) return rc;
     if (tev) {
       HIP_OK(hipEventRecord(tev[2], b->stream));
       HIP_OK(hipEventRecord(tev[3], b->stream));
@@ -3905,7 +4396,7 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, status,
                      iters, b->d_diag, b->d_summary, loop_ctl(b), b->loop_xa,
                      cached ? (const int32_t *)b->d_ctr : nullptr,
-                     cached ? (const int32_t *)b->d_wl2 : nullptr, b->d_err);
+                     cached ? (const int32_t *)b->d_wl2 : nullptr, b->d_err, 0);
   HIP_OK(hipGetLastError());
   return PH_OK;
 }
@@ -4169,6 +4660,150 @@ int ph_loop_pass(ph_batch_t b) {
                        p.iters, p.pobj, p.dbound, &p.opts);
 }
 
+// ph_loop_run's persistent path applies: one rank, the one-wave cached warm
+// solve (register polish shape), the device loop's Compute_Xbar sums bound
+// to this pass, and the owned scenarios' data fit one block's LDS on a
+// resident grid (PHGPU_PERSIST=1: on, measurement hook).  Sets up the grid,
+// the LDS size and the partial buffers on first use.
+static int loop_persist_setup(ph_batch *b, bool *ok) {
+  *ok = false;
+  // opt-in (PHGPU_PERSIST=1, read per call: tests compare both paths).  At F2
+  // it measured no faster than the per-pass kernels (51.0 against 51.2 us per
+  // pass): two grid barriers cost 7.7 + ~10 us on the 8-XCD part and the
+  // solve phase runs one wave per SIMD (the polish's register budget), 2.4 us
+  // per owned scenario (tools/loop_prof.py, profiles/r04/loop_prof_f2.txt)
+  const char *env = std::getenv("PHGPU_PERSIST");
+  const bool env_on = env && std::atoi(env) != 0;
+  const ph_loop_pass_args &p = b->pass;
+  if (!env_on || p.conv_part || b->mid || !polish_fits(b) || !b->d_sb || !b->d_cache || !p.opts.polish ||
+      !p.opts.warm_start || b->K <= 0 || b->K > RG_K || b->n > WAVE || b->m > WAVE || p.G <= 0 ||
+      p.G > 512 || b->loop_xa.G != p.G || b->loop_xa.C <= 0 || b->loop_xa.x != p.x ||
+      b->loop_xa.out != p.sums)
+    return PH_OK;
+  if (b->loop_grid == 0 || b->loop_G != p.G) {
+    int cus = 0, dev = 0, per_cu = 0;
+    HIP_OK(hipGetDevice(&dev));
+    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int NB = std::max(1, std::min(cus, (b->S + LOOP_WPB - 1) / LOOP_WPB));
+    const int NW = NB * LOOP_WPB;
+    const int spw = (b->S + NW - 1) / NW;
+    const LoopLds lay = loop_lds(b->n, b->m, b->nnz, b->K, p.G, b->CW, spw);
+    const size_t bytes = sizeof(double) * (size_t)lay.total;
+    if (bytes > 160 * 1024) return PH_OK;
+    HIP_OK(hipFuncSetAttribute((const void *)loop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, loop_kernel, LOOP_WPB * WAVE, bytes));
+    if (per_cu < 1) return PH_OK;  // cannot be resident: the per-pass kernels
+    if (b->d_lpart) HIP_OK(hipFree(b->d_lpart));
+    b->d_lpart = nullptr;
+    if (int rc = dalloc(&b->d_lpart, (size_t)NB * (2 * p.G + 3))) return rc;
+    if (!b->d_lbar)
+      if (int rc = dalloc(&b->d_lbar, 2)) return rc;
+    b->loop_grid = NB;  // <= CUs x per_cu: every block resident
+    b->loop_spw = spw;
+    b->loop_G = p.G;
+    b->loop_lds_bytes = bytes;
+  }
+  *ok = true;
+  return PH_OK;
+}
+
+__global__ void loop_prep_kernel(LoopCtl *c, int32_t *bar, int iters, int first) {
+  bar[0] = 0;
+  bar[1] = 0;
+  if (first) c->iter_end = c->iter + iters;
+}
+
+int ph_loop_persistent(ph_batch_t b) {
+  if (!b || !b->loop_on || !b->pass_bound) return 0;
+  bool ok = false;
+  if (loop_persist_setup(b, &ok)) return 0;
+  return ok ? 1 : 0;
+}
+
+int ph_loop_read_timing(ph_batch_t b, double *out) {
+  if (!b || !out) return fail(PH_EINVAL, "ph_loop_read_timing: bad arguments");
+  LoopCtl h;
+  HIP_OK(hipMemcpyAsync(&h, b->d_ctl, sizeof(h), hipMemcpyDeviceToHost, b->stream));
+  HIP_OK(hipStreamSynchronize(b->stream));
+  out[0] = out[1] = 0.0;
+  for (size_t i = 0; i + 1 < b->pev_used; i += 2) {
+    if (b->pkind[i] != 2) continue;
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, b->pev[i], b->pev[i + 1]));
+    out[0] += 1.0;
+    out[1] += ms;
+  }
+  out[2] = (double)h.lpasses;
+  return PH_OK;
+}
+
+int ph_loop_run(ph_batch_t b, int32_t iters) {
+  if (!b || !b->loop_on || !b->pass_bound)
+    return fail(PH_EINVAL, "ph_loop_run: loop not enabled or no pass bound");
+  if (iters <= 0) return PH_OK;
+  bool persist = false;
+  if (int rc = loop_persist_setup(b, &persist)) return rc;
+  if (!persist) {  // the per-pass kernels
+    for (int i = 0; i < iters; ++i)
+      if (int rc = ph_loop_pass(b)) return rc;
+    return PH_OK;
+  }
+  const ph_loop_pass_args &p = b->pass;
+  SolveArgs a;
+  fill_solve_args(b, p.W, p.rho, p.xbar, p.w_on, p.prox_on, p.x, p.y, p.omega, p.status, p.iters, p.pobj,
+                  p.dbound, &p.opts, a);
+  if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_loop_run: bad options");
+  const size_t lds = solve_lds_bytes(b);
+  if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_loop_run: scenario does not fit in LDS");
+  if (int rc = ensure_pdhg_grid(b, lds)) return rc;
+  a.hint = b->d_hint;
+  a.hint_ok = b->d_hint_ok;
+  a.wl = b->d_wl;
+  a.wl2 = b->d_wl2;
+  a.ul = nullptr;
+  LoopArgs L;
+  L.a = a;
+  L.a.prof = nullptr;
+  L.sums = b->loop_xa.out;  // (== p.sums)
+  L.G = p.G;
+  L.gid = p.gid;
+  L.rho = p.rho;
+  L.wc = p.w_coeff;
+  L.pc = b->loop_xa.pc;
+  L.xbar = p.xbar;
+  L.xsqbar = p.xsqbar;
+  L.W = p.W;
+  L.absdiff = p.absdiff;
+  L.wconv = p.wconv;
+  L.hist = p.conv_hist;
+  L.ctl = b->d_ctl;
+  L.ctr = b->d_ctr;
+  L.part_x = b->d_lpart;
+  L.part_c = b->d_lpart + (size_t)b->loop_grid * (2 * p.G + 2);
+  L.bar = b->d_lbar;
+  L.spw = b->loop_spw;
+  L.prof = b->d_prof;
+  // rounds of (persistent passes, the tail of a pass that needed one, its
+  // summary); a round whose loop_kernel ran to iter_end leaves the rest idle
+  constexpr int ROUNDS = 4;
+  const int post_g = b->loop_xa.G * std::max(1, b->loop_xa.C);
+  for (int r = 0; r < ROUNDS; ++r) {
+    hipLaunchKernelGGL(loop_prep_kernel, dim3(1), dim3(1), 0, b->stream, b->d_ctl, b->d_lbar, (int)iters,
+                       r == 0 ? 1 : 0);
+    if (int rc = phase_event(b, 2)) return rc;
+    hipLaunchKernelGGL(loop_kernel, dim3(b->loop_grid), dim3(LOOP_WPB * WAVE), b->loop_lds_bytes, b->stream, L);
+    HIP_OK(hipGetLastError());
+    if (int rc = phase_event(b, -1)) return rc;
+    if (int rc = launch_tail(b, a, lds)) return rc;
+    hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, p.status, p.iters,
+                       b->d_diag, b->d_summary, b->d_ctl, b->loop_xa, (const int32_t *)b->d_ctr,
+                       (const int32_t *)b->d_wl2, b->d_err, 1);
+    HIP_OK(hipGetLastError());
+  }
+  return PH_OK;
+}
+
 int ph_loop_status(ph_batch_t b, int64_t *out) {
   if (!b || !out) return fail(PH_EINVAL, "ph_loop_status: bad arguments");
   LoopCtl h;
@@ -4216,6 +4851,7 @@ int ph_batch_read_timing(ph_batch_t b, double *out) {
   for (size_t i = 0; i + 1 < b->pev_used; i += 2) {
     float ms = 0.f;
     HIP_OK(hipEventElapsedTime(&ms, b->pev[i], b->pev[i + 1]));
+    if (b->pkind[i] == 2) continue;  // (loop_kernel: ph_loop_read_timing)
     const int k = b->pkind[i] == 1 ? 1 : 0;
     out[4 + 2 * k] += 1.0;
     out[5 + 2 * k] += ms;
@@ -4262,7 +4898,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
                   b->d_ctl, b->d_sym, b->d_sym16, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
-                  b->d_bws,
+                  b->d_bws, b->d_lpart, b->d_lbar,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

@@ -346,6 +346,23 @@ class DeviceBatch:
         """One device-loop pass (ph_loop_pass): one call per PH iteration."""
         _native.check(self.lib.ph_loop_pass(self.handle), "ph_loop_pass")
 
+    def loop_run(self, iters):
+        """Up to `iters` device-loop passes in one call (ph_loop_run): on one
+        rank a persistent launch when the batch qualifies and PHGPU_PERSIST=1,
+        else `iters` ph_loop_pass calls inside the library."""
+        _native.check(self.lib.ph_loop_run(self.handle, int(iters)), "ph_loop_run")
+
+    def loop_persistent(self):
+        """True when loop_run takes the persistent path for the bound pass."""
+        return bool(self.lib.ph_loop_persistent(self.handle))
+
+    def loop_read_timing(self):
+        """(loop_kernel launches, their total ms, passes they ran) while timing."""
+        out = np.zeros(3, dtype=np.float64)
+        _native.check(self.lib.ph_loop_read_timing(self.handle, out.ctypes.data_as(_native._c_ptr)),
+                      "ph_loop_read_timing")
+        return float(out[0]), float(out[1]), int(out[2])
+
     def loop_status(self):
         """(stop, iter, not-optimal solves, solves, PDHG iters sum, max, polished,
         cached); synchronises.  stop: 0 running, 1 converged, 2 iteration limit."""

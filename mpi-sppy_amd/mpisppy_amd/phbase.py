@@ -689,6 +689,17 @@ class PHBase(SPBase):
             self._allreduce(self.xpass)
         self.batch.loop_pass()
 
+    def _device_chunk(self, kw, chunk):
+        """`chunk` passes.  One rank: ONE library call (ph_loop_run: a
+        persistent launch that keeps the scenarios' data in LDS across the
+        passes when the batch qualifies, else the per-pass kernels); several
+        ranks: one ph_loop_pass per pass after its allreduce."""
+        if self.comm.size == 1:
+            self.batch.loop_run(chunk)
+        else:
+            for _ in range(chunk):
+                self._device_iteration(kw)
+
     def _bind_pass(self, kw):
         """ph_loop_bind_pass: the device loop's per-pass arguments, once."""
         b = self.batch
@@ -740,8 +751,7 @@ class PHBase(SPBase):
                 if graph is not None:
                     graph.replay()
                 else:
-                    for _ in range(chunk):
-                        self._device_iteration(kw)
+                    self._device_chunk(kw, chunk)
                 st = b.loop_status()
                 dt = time.perf_counter() - t0
                 stop, it, nonopt, nsolves, it_sum, it_max, npol, ncache = st
@@ -805,7 +815,7 @@ class PHBase(SPBase):
         with torch.cuda.graph(g):
             b.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
             try:
-                for _ in range(chunk):
+                for _ in range(chunk):  # (the per-pass kernels: captured as a graph)
                     self._device_iteration(kw)
             finally:
                 b.set_stream(b.stream_handle)

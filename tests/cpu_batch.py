@@ -147,6 +147,13 @@ class CPUBatch:
                 self.loop_backup_status(ss, ds)
         self.solve(p["W"], p["rho"], p["xbar"], p["w_on"], p["prox_on"])
 
+    def loop_run(self, iters):
+        """ph_loop_run semantics: up to `iters` passes (the stop flag ends it)."""
+        for _ in range(int(iters)):
+            if self._stopped():
+                break
+            self.loop_pass()
+
     def loop_status(self):
         c = self._ctl
         return (c["stop"], c["iter"], *c["acc"])

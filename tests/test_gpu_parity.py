@@ -943,3 +943,60 @@ def test_wxbar_files_from_the_hip_path_match_oracle_and_resume(tmp_path):
     ph3.ph_main()
     assert _rel(ph2.W.cpu().numpy(), ph3.W.cpu().numpy()) < 1e-6
     assert _rel(ph2.xbar.cpu().numpy(), ph3.xbar.cpu().numpy()) < 1e-6
+
+
+def _loop_run(model, S, limit, thresh, persist, monkeypatch):
+    """Iter0 + run_device_loop(0, limit) with PHGPU_PERSIST=persist; returns
+    (iterations, stop, conv history, xbar, W, x, loop_kernel launches, its passes)."""
+    from mpisppy_amd.opt.ph import PH
+    monkeypatch.setenv("PHGPU_PERSIST", persist)
+    if model == "farmer":
+        from mpisppy_amd.examples import farmer
+        ph = PH(dict(_opts(PHIterLimit=limit, defaultPHrho=1.0, convthresh=thresh)),
+                [f"scen{i}" for i in range(S)], farmer.scenario_creator)
+    else:
+        from mpisppy_amd.examples import hydro
+        names, nodes = hydro.all_names_and_nodes((3, 3))
+        ph = PH(dict(_opts(PHIterLimit=limit, defaultPHrho=1.0, convthresh=thresh,
+                           branching_factors=[3, 3])), names, hydro.scenario_creator,
+                all_nodenames=nodes, scenario_creator_kwargs={"branching_factors": [3, 3]})
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    ph._create_solvers()
+    ph.Iter0()
+    b = ph.batch
+    b.set_timing(True)
+    stop, it = ph.run_device_loop(0, limit, thresh, chunk=16)
+    launches, _, passes = b.loop_read_timing()
+    b.set_timing(False)
+    return (it, stop, ph.conv_hist[:it].cpu().numpy().copy(), ph.xbar.cpu().numpy().copy(),
+            ph.W.cpu().numpy().copy(), b.x.cpu().numpy().copy(), launches, passes)
+
+
+@pytest.mark.parametrize("model,S,limit,auto", [("farmer", 1000, 120, True), ("farmer", 37, 60, False)])
+def test_persistent_loop_matches_per_pass_kernels(model, S, limit, auto, monkeypatch):
+    """ph_loop_run's persistent launch (loop_kernel: the scenarios' data
+    resident in LDS, two grid barriers per pass, a miss polished by the wave
+    that owns it, a polish failure finished by the queued tail + post-solve
+    kernels) against the per-pass kernels from PH iteration 1 (whose misses
+    and tails are many): the same iterations, conv history, x-bar, W and x up
+    to the summation order of Compute_Xbar's sums and of conv.  Farmer 1000
+    stops at a convthresh placed in a clear drop of the per-pass run's conv
+    history past the middle (so round-off cannot move the stop); farmer 37
+    has waves without scenarios.  (Hydro's K = 8 nonants per scenario exceed
+    the register polish's K <= 4: it keeps the per-pass kernels.)"""
+    thresh = -1.0
+    if auto:
+        c = _loop_run(model, S, limit, -1.0, "0", monkeypatch)[2]
+        k = next(k for k in range(limit // 2, limit) if c[k] < 0.99 * c[:k].min())
+        thresh = 0.5 * (c[k] + c[:k].min())
+    p = _loop_run(model, S, limit, thresh, "1", monkeypatch)
+    q = _loop_run(model, S, limit, thresh, "0", monkeypatch)
+    assert p[6] > 0 and p[7] > 0, "the persistent path did not run"
+    assert q[6] == 0 and q[7] == 0
+    assert p[0] == q[0] and p[1] == q[1]
+    if auto:
+        assert p[1] == 1 and p[0] == k + 1
+    assert np.allclose(p[2], q[2], rtol=1e-8, atol=1e-12)
+    for a, b_ in zip(p[3:6], q[3:6]):
+        assert _rel(a, b_) < 1e-8

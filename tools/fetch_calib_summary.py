@@ -16,7 +16,8 @@ import sys
 
 def rows(d, counter):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-    out = [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter]
+    out = [r for r in csv.DictReader(open(f))
+           if r["Counter_Name"] == counter and not r["Kernel_Name"].startswith("__amd_rocclr")]
     out.sort(key=lambda r: int(r["Dispatch_Id"]))
     return [(r["Kernel_Name"], float(r["Counter_Value"])) for r in out]
 
