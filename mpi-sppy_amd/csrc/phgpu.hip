@@ -4859,6 +4859,24 @@ int ph_batch_read_timing(ph_batch_t b, double *out) {
   return PH_OK;
 }
 
+// Debug (not in phgpu.h): the recorded phase launches one by one while
+// timing is on: out[2*i] = kind (0 mid_kernel / big_kernel, 1 polish, 2
+// loop_kernel), out[2*i+1] = ms; returns the count (<= cap) or < 0.  ctr[16]
+// (optional): the mid-size phase list counts / queue counters (d_mctr).
+int ph_debug_phase_times(ph_batch_t b, double *out, int32_t cap, int32_t *ctr) {
+  if (!b || !out || cap < 0) return -fail(PH_EINVAL, "ph_debug_phase_times: bad arguments");
+  HIP_OK(hipStreamSynchronize(b->stream));
+  int k = 0;
+  for (size_t i = 0; i + 1 < b->pev_used && k < cap; i += 2, ++k) {
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, b->pev[i], b->pev[i + 1]));
+    out[2 * k] = b->pkind[i];
+    out[2 * k + 1] = ms;
+  }
+  if (ctr && b->d_mctr) HIP_OK(hipMemcpy(ctr, b->d_mctr, 16 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return k;
+}
+
 // Debug (not in phgpu.h): phase clocks of pdhg_kernel's warm polish, in
 // 100 MHz ticks, and exit-reason counters of the mid-size polish (slots in
 // solve_mid.inc).  on != 0 clears and enables, on == 0 disables; read copies

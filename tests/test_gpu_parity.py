@@ -1000,3 +1000,74 @@ def test_persistent_loop_matches_per_pass_kernels(model, S, limit, auto, monkeyp
     assert np.allclose(p[2], q[2], rtol=1e-8, atol=1e-12)
     for a, b_ in zip(p[3:6], q[3:6]):
         assert _rel(a, b_) < 1e-8
+
+
+def test_uc_lp_relaxation_matches_oracle():
+    """BASELINE config 4's model: the LP relaxation of
+    paperruns/larger_uc/ReferenceModel_OK.py on the WECC-240 data
+    (examples/uc.py; 56,869 columns, 69,902 rows per scenario: the big path
+    with the row duals in the workspace slice), Scenario1..3 of
+    1000scenarios_wind with the reference's rho setter (uc_funcs.py:94-112).
+    PARITY UNPINNED: no reference file holds UC LP-relaxation values, and
+    this is ReferenceModel's formulation, not egret's; the oracle is the
+    independent restatement oracle/models.uc solved by HiGHS simplex
+    (tests/golden/uc_lp_values.json, tests/golden/make_uc_golden.py).
+    Iter0: every scenario's outer bound to 1e-7 of its LP value, the trivial
+    bound to 1e-7.  Two PH iterations (host loop): Compute_Xbar / Update_W
+    against the oracle's restatement on the same nonants to 1e-12, every
+    prox-QP solution a KKT point of its QP (built from the batch's own data,
+    which tests/test_abi_layout.py pins to the oracle's LP) at 1e-7."""
+    import json
+    import os
+    import scipy.sparse as sp
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import uc
+    from oracle.solve import kkt_residual
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "uc_lp_values.json")))
+    names = uc.all_scenario_names(3)
+    opts = _opts(PHIterLimit=2, defaultPHrho=1.0, convthresh=-1.0)
+    ph = PH(dict(opts), names, uc.scenario_creator, rho_setter=uc.scenario_rhos)
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    tb = ph.Iter0()
+    b = ph.batch
+    S, n, m = b.S, b.n, b.m
+    assert (n, m) == (56869, 69902)
+    assert np.all(b.status.cpu().numpy() == 0)
+    vals = np.array([gold["values"][nm] for nm in names])
+    ob = b.dbound.cpu().numpy() + b.const.cpu().numpy()
+    assert np.all(np.abs(ob - vals) <= 1e-7 * np.abs(vals)), (ob, vals)
+    assert abs(tb - vals.mean()) <= 1e-7 * abs(vals.mean()), (tb, vals.mean())
+    orc = OraclePH(dict(opts), [om.uc(nm) for nm in names])
+    bd = ph.batch_data
+    cols = bd.nonant_cols
+    rho = ph.rho.view(ph.K, S).cpu().numpy()
+    for s in range(S):
+        orc.rho[s] = rho[:, s].copy()
+    for k in range(1, 3):
+        ph.Compute_Xbar()
+        ph.Update_W(False)
+        X = b.x.view(n, S).cpu().numpy()
+        for s in range(S):
+            xo = np.zeros(orc.scens[s].A.shape[1])
+            xo[orc.scens[s].nonant_idx] = X[cols, s]
+            orc.x[s] = xo
+        orc.Compute_Xbar()
+        orc.Update_W()
+        assert _rel(ph.xbar.view(ph.K, S).cpu().numpy().T, np.array(orc.xbar)) < 1e-12
+        assert _rel(ph.W.view(ph.K, S).cpu().numpy().T, np.array(orc.W)) < 1e-12
+        ph.solve_loop(solver_options=ph.current_solver_options)
+        assert np.all(b.status.cpu().numpy() == 0), k
+        X = b.x.view(n, S).cpu().numpy()
+        Y = b.y.view(m, S).cpu().numpy()
+        W = ph.W.view(ph.K, S).cpu().numpy()
+        xb = ph.xbar.view(ph.K, S).cpu().numpy()
+        for s in range(S):
+            A = sp.csr_matrix((bd.vals[:, s], bd.col_idx, bd.row_ptr), shape=(m, n))
+            g = bd.c[:, s].copy()
+            q = np.zeros(n)
+            g[cols] += W[:, s] - rho[:, s] * xb[:, s]
+            q[cols] += rho[:, s]
+            pv, dv = kkt_residual(X[:, s], Y[:, s], g, q, A, bd.rl[:, s], bd.ru[:, s], bd.l[:, s],
+                                  bd.u[:, s])
+            assert max(pv, dv) < 1e-7, (k, s, pv, dv)

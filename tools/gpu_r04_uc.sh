@@ -7,5 +7,5 @@ O=$R/gpurun_out
 mkdir -p $O
 cd $R
 export TMPDIR=/tmp
-timeout -k 10 400 python -u tools/uc_probe.py 3 2 > $O/uc_probe3.txt 2>&1 || { echo "uc probe failed"; tail -30 $O/uc_probe3.txt; exit 1; }
+timeout -k 10 600 python -u tools/uc_probe.py 3 1 5000 > $O/uc_probe3.txt 2>&1 || { echo "uc probe failed"; tail -30 $O/uc_probe3.txt; exit 1; }
 cat $O/uc_probe3.txt

@@ -4,7 +4,7 @@ Iter0 of S scenarios through the big path (y in the workspace slice: m =
 the oracle's HiGHS LP values (first 3 scenarios), then NIT PH iterations
 with the reference's rho setter (uc_funcs.py:94-112).
 
-    python tools/uc_probe.py S NIT [max_iters]
+    python tools/uc_probe.py S NIT [max_iters] [tol]
 """
 import os
 import sys
@@ -23,6 +23,7 @@ from mpisppy_amd.examples import uc  # noqa: E402
 S = int(sys.argv[1])
 NIT = int(sys.argv[2])
 MAXIT = int(sys.argv[3]) if len(sys.argv) > 3 else 200000
+TOL = float(sys.argv[4]) if len(sys.argv) > 4 else 1e-9
 t0 = time.time()
 
 
@@ -30,9 +31,20 @@ def say(m):
     print(f"[uc_probe {time.time() - t0:7.1f}] {m}", flush=True)
 
 
+def _heartbeat():  # the solves block in one library call; keep the log moving
+    while True:
+        time.sleep(30)
+        print(f"[uc_probe {time.time() - t0:7.1f}] ...", flush=True)
+
+
+import threading  # noqa: E402
+threading.Thread(target=_heartbeat, daemon=True).start()
+
+
 opts = {"solvername": "mi355x_pdhg", "PHIterLimit": NIT, "defaultPHrho": 1.0, "convthresh": -1.0,
-        "verbose": False, "display_progress": False, "iter0_solver_options": {"pdhg_max_iters": MAXIT},
-        "iterk_solver_options": {"pdhg_max_iters": MAXIT}, "device_loop": False}
+        "verbose": False, "display_progress": False,
+        "iter0_solver_options": {"pdhg_max_iters": MAXIT, "pdhg_tol": TOL},
+        "iterk_solver_options": {"pdhg_max_iters": MAXIT, "pdhg_tol": TOL}, "device_loop": False}
 names = uc.all_scenario_names(S)
 ph = PH(opts, names, uc.scenario_creator, rho_setter=uc.scenario_rhos)
 ph.PH_Prep()
@@ -54,7 +66,8 @@ say(f"Iter0 {dt:.2f} s: trivial bound {tb:.6f}, statuses {np.bincount(st, minlen
     f"{it.mean():.0f} max {it.max()}, how {np.bincount(d[:, 4].astype(int), minlength=4)}")
 print("  final errors of the first scenarios:", d[:3, :3], flush=True)
 nt, _, _, _, nk, k_ms, np_, p_ms = b.read_timing_full()
-say(f"  big_kernel {nk} launches {k_ms:.1f} ms, polish {np_} launches {p_ms:.1f} ms")
+say(f"  big_kernel {nk} launches {k_ms:.1f} ms, polish {np_} launches {p_ms:.1f} ms; "
+    f"{k_ms / max(it.sum() / S, 1):.4f} ms per PDHG step (per scenario, in parallel)")
 if S <= 8:
     from oracle import models as om
     from oracle.solve import _highs_solve
