@@ -330,6 +330,15 @@ __device__ __forceinline__ void dev_fail(int32_t *err, int code, int v0, int v1)
   }
 }
 
+// Agent-scope (cross-XCD) publish / subscribe of a double: the partials of
+// the multi-block reductions (write-through stores, L1-bypassing loads).
+__device__ __forceinline__ void pub(double *p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double sub(const double *p) {
+  return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Append s to a work list of capacity S (a list never holds more than S
 // entries: a ticket past it is an invariant violation, recorded, and the
 // store skipped).
@@ -2524,12 +2533,6 @@ __global__ void __launch_bounds__(1024) segment_sum_kernel(
 // stores (coherent across the XCDs' L2s): no release fence, which on gfx950
 // writes back the whole L2 and costs microseconds per block.
 // ------------------------------------------------------------------------
-__device__ __forceinline__ void pub(double *p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double sub(const double *p) {
-  return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 // The publishing stores of thread 0 precede its ticket: they are complete
 // (vmcnt drained) before the ticket's atomic is issued.
 __device__ __forceinline__ bool last_block(int32_t *ticket) {
@@ -3255,6 +3258,9 @@ struct ph_batch {
   size_t big_lds_bytes = 0;     // LDS of big_kernel (y + scratch)
   bool big_ylds = true;         // big_kernel<true>: y in LDS; <false>: y in the slice (m > ~20,000)
   int big_grid = 0;             // resident blocks of the big phase kernels
+  int big_tgrid = 0;            // big_kernel's launch grid (teams: every resident block)
+  int32_t *d_teambar = nullptr; // [big_tgrid + 1] team barrier counters, abort flag
+  double *d_teampart = nullptr; // team reduction partials
   // persistent device loop (ph_loop_run, loop_kernel)
   int loop_grid = 0, loop_spw = 0, loop_G = 0;  // resident blocks, scenario slots per wave, for G
   size_t loop_lds_bytes = 0;
@@ -3977,6 +3983,27 @@ static int big_init(ph_batch *b) {
       (rc = dalloc(&b->d_vals_t, (size_t)b->S * b->nnz)) || (rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) ||
       (rc = dalloc(&b->d_mctr, 16)))
     return rc;
+  // teams (a short PDHG list shares the resident grid, BigTeam): the PDHG
+  // launches go over every resident block; PHGPU_BIG_TEAMS=0: off
+  // (measurement hook), as is a capped grid (PHGPU_MID_GRID: the parity
+  // tests of the work-queue path)
+  b->big_tgrid = grid;
+  b->bg.team_bar = b->bg.team_abort = nullptr;
+  b->bg.team_part = nullptr;
+  const char *te = std::getenv("PHGPU_BIG_TEAMS");
+  int per_cu_t = 0;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, big_team_kernel, BIG_BLOCK, BIG_SMALL_LDS));
+  if (!(te && std::atoi(te) == 0) && !mid_grid_cap() && per_cu_t >= 1) {
+    // every block of the launch resident: a team's barrier needs all of it
+    const int tg = std::min(std::max(1, per_cu), per_cu_t) * std::max(1, cus);
+    if ((rc = dalloc(&b->d_teambar, (size_t)tg + 1)) ||
+        (rc = dalloc(&b->d_teampart, (size_t)tg * 2 * BIG_TEAM_MAX * 16)))
+      return rc;
+    b->big_tgrid = tg;
+    b->bg.team_bar = b->d_teambar;
+    b->bg.team_abort = b->d_teambar + tg;
+    b->bg.team_part = b->d_teampart;
+  }
   b->bg.ws_g = b->d_bws;
   b->bg.vals_t = b->d_vals_t;
   b->mid_grid = b->mid_pgrid = grid;
@@ -4036,8 +4063,19 @@ static int mid_init(ph_batch *b) {
 //   polish (those trial points)   PDHG (hand on at 1e-6)   polish
 //   PDHG  (to tolerance or the iteration limit)
 // then the summary kernel.  Without the polish option: one PDHG phase.
+// The big path's LDL' polish is one workgroup's level-scheduled
+// factorisation per round: past this many update contributions (UC: 58M,
+// ~0.6 s per factorisation, 7.5 s per polish launch, and it did not accept
+// a UC LP) the solve is PDHG only (teams make that fast for short lists).
+// PHGPU_BIG_POLISH_MAX_CONTRIB: measurement hook.
+static long big_polish_max_contrib() {
+  const char *e = std::getenv("PHGPU_BIG_POLISH_MAX_CONTRIB");
+  return e ? std::atol(e) : 16L << 20;
+}
+
 static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   a.polish = opts ? opts->polish : 1;
+  if (b->big && b->sym.ncontrib > big_polish_max_contrib()) a.polish = 0;
   a.cache = nullptr;
   a.wl = nullptr;
   if (int rc = mid_init(b)) return rc;
@@ -4085,12 +4123,17 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     const MidPhase ph{in, cin, out, cout, q, exit_err, first, 0, hand_at_limit};
     if (int rc = phase_event(b, 0)) return rc;
     if (b->big) {
+      if (b->bg.team_bar)  // the teams' barrier counters and abort flag
+        hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_teambar, b->big_tgrid + 1);
       if (b->big_ylds)
-        hipLaunchKernelGGL(big_kernel<true>, dim3(b->big_grid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
+        hipLaunchKernelGGL(big_kernel<true>, dim3(b->big_tgrid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
                            a, b->bg, ph);
       else
-        hipLaunchKernelGGL(big_kernel<false>, dim3(b->big_grid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
+        hipLaunchKernelGGL(big_kernel<false>, dim3(b->big_tgrid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
                            a, b->bg, ph);
+      if (b->bg.team_bar)  // (exits at once unless the phase's list is short)
+        hipLaunchKernelGGL(big_team_kernel, dim3(b->big_tgrid), dim3(BIG_BLOCK), BIG_SMALL_LDS, b->stream, a,
+                           b->bg, ph);
       HIP_OK(hipGetLastError());
       return phase_event(b, -1);
     }
@@ -4916,7 +4959,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
                   b->d_ctl, b->d_sym, b->d_sym16, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
-                  b->d_bws, b->d_lpart, b->d_lbar,
+                  b->d_bws, b->d_lpart, b->d_lbar, b->d_teambar, b->d_teampart,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

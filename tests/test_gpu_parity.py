@@ -1013,7 +1013,7 @@ def test_uc_lp_relaxation_matches_oracle():
     independent restatement oracle/models.uc solved by HiGHS simplex
     (tests/golden/uc_lp_values.json, tests/golden/make_uc_golden.py).
     Iter0: every scenario's outer bound to 1e-7 of its LP value, the trivial
-    bound to 1e-7.  Two PH iterations (host loop): Compute_Xbar / Update_W
+    bound to 1e-7.  One PH iteration (host loop): Compute_Xbar / Update_W
     against the oracle's restatement on the same nonants to 1e-12, every
     prox-QP solution a KKT point of its QP (built from the batch's own data,
     which tests/test_abi_layout.py pins to the oracle's LP) at 1e-7."""
@@ -1025,7 +1025,11 @@ def test_uc_lp_relaxation_matches_oracle():
     from oracle.solve import kkt_residual
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "uc_lp_values.json")))
     names = uc.all_scenario_names(3)
-    opts = _opts(PHIterLimit=2, defaultPHrho=1.0, convthresh=-1.0)
+    opts = _opts(PHIterLimit=1, defaultPHrho=1.0, convthresh=-1.0)
+    # PDHG only (the factorisation is past the big polish's size limit):
+    # Scenario1's LP takes ~612k steps, the prox-QPs ~170k
+    opts["iter0_solver_options"] = {"pdhg_max_iters": 1000000}
+    opts["iterk_solver_options"] = {"pdhg_max_iters": 400000}
     ph = PH(dict(opts), names, uc.scenario_creator, rho_setter=uc.scenario_rhos)
     ph.PH_Prep()
     ph.subproblem_creation()
@@ -1044,7 +1048,7 @@ def test_uc_lp_relaxation_matches_oracle():
     rho = ph.rho.view(ph.K, S).cpu().numpy()
     for s in range(S):
         orc.rho[s] = rho[:, s].copy()
-    for k in range(1, 3):
+    for k in range(1, 2):
         ph.Compute_Xbar()
         ph.Update_W(False)
         X = b.x.view(n, S).cpu().numpy()
@@ -1071,3 +1075,37 @@ def test_uc_lp_relaxation_matches_oracle():
             pv, dv = kkt_residual(X[:, s], Y[:, s], g, q, A, bd.rl[:, s], bd.ru[:, s], bd.l[:, s],
                                   bd.u[:, s])
             assert max(pv, dv) < 1e-7, (k, s, pv, dv)
+
+
+def test_big_teams_match_one_block(monkeypatch):
+    """The big path's teams (big_team_kernel: a short PDHG list shares the
+    resident grid, T blocks per scenario, team barriers and rank-ordered
+    reductions) against the one-block kernel (PHGPU_BIG_TEAMS=0) on F4's
+    scenario shape, 3 scenarios (teams of 64 for every phase): Iter0 and two
+    PH iterations give the same statuses, PDHG step counts, bounds and x.
+    (The reductions' summation order differs, so the PDHG trajectories agree
+    to round-off, not bit for bit.)"""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    names = ["scen22", "scen7", "scen3"]
+    res = []
+    for teams in ("1", "0"):
+        monkeypatch.setenv("PHGPU_BIG_TEAMS", teams)
+        opts = _opts(PHIterLimit=2, defaultPHrho=1.0, convthresh=-1.0, device_loop=False)
+        ph = PH(dict(opts), names, farmer.scenario_creator, scenario_creator_kwargs={"crops_multiplier": 1000})
+        ph.PH_Prep()
+        ph.subproblem_creation()
+        tb = ph.Iter0()
+        b = ph.batch
+        out = [tb, b.status.cpu().numpy().copy(), b.x.cpu().numpy().copy()]
+        for _ in range(2):
+            ph.Compute_Xbar()
+            ph.Update_W(False)
+            ph.solve_loop(solver_options=ph.current_solver_options)
+        out += [b.status.cpu().numpy().copy(), b.x.cpu().numpy().copy(), ph.Eobjective()]
+        res.append(out)
+    (t1, s1, x1, s1b, x1b, e1), (t0, s0, x0, s0b, x0b, e0) = res
+    assert np.all(s1 == 0) and np.all(s0 == 0) and np.all(s1b == 0) and np.all(s0b == 0)
+    assert abs(t1 - t0) <= 1e-9 * abs(t0)
+    assert abs(e1 - e0) <= 1e-9 * abs(e0)
+    assert _rel(x1b, x0b) < 1e-6
