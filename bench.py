@@ -466,6 +466,65 @@ def sslp_config(args, world, PH, opts):
             "pdhg_steps_per_solve": round(st[4] / max(st[3], 1), 1), "pdhg_steps_max": st[5]}
 
 
+def uc_config(args, world, PH, opts):
+    """BASELINE config 4's model at a reduced scenario count: the LP
+    relaxation of paperruns/larger_uc/ReferenceModel_OK.py on the WECC-240
+    data (examples/uc.py: n = 56,869, m = 69,902, nnz = 240,508 per scenario;
+    Scenario1.. of 1000scenarios_wind, the reference's rho setter), --uc-scens
+    per rank.  The big path with y in the workspace slice, PDHG only (the
+    LDL' factorisation, 58M update contributions, is past the big polish's
+    size limit) on teams of blocks (a short list shares the resident grid).
+    Iter0 (LPs to 1e-9), then --uc-steps PH iterations (prox-QPs, host
+    loop).  1,000 scenarios are out of reach of a bench run on this path: at
+    ~400k PDHG steps per LP one block per scenario streams ~10 MB per step."""
+    from mpisppy_amd.examples import uc
+    S = args.uc_scens * world
+    o = dict(opts)
+    o["iter0_solver_options"] = {"pdhg_max_iters": 1000000}
+    o["iterk_solver_options"] = {"pdhg_max_iters": 400000}
+    o["device_loop"] = False
+    ph = PH(o, uc.all_scenario_names(S), uc.scenario_creator, rho_setter=uc.scenario_rhos)
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    ph._create_solvers()
+    b = ph.batch
+    torch.cuda.synchronize()
+    _progress("UC Iter0")
+    t0 = time.perf_counter()
+    tb = ph.Iter0()
+    torch.cuda.synchronize()
+    t_iter0 = time.perf_counter() - t0
+    it0 = b.iters.cpu().numpy()
+    nonopt0 = int((b.status != 0).sum().item())
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps = []
+    for _ in range(args.uc_steps):
+        ph.Compute_Xbar()
+        ph.Update_W(False)
+        ph.solve_loop(solver_options=ph.current_solver_options)
+        steps.append(float(b.iters.float().mean().item()))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    d = torch.tensor([dt], dtype=torch.float64, device=_red_dev())
+    if world > 1:
+        dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    dt = float(d.item())
+    return {"workload": f"UC LP relaxation (ReferenceModel_OK.py, WECC-240), {S} scenarios "
+                        f"({args.uc_scens} per GPU), n={b.n}, m={b.m}, nnz={b.nnz} per scenario, "
+                        "reference rho setter",
+            "iter0_s": round(t_iter0, 2), "iter0_not_optimal": nonopt0, "trivial_bound": tb,
+            "iter0_pdhg_steps_mean": round(float(it0.mean()), 1), "iter0_pdhg_steps_max": int(it0.max()),
+            "ph_iterations": args.uc_steps,
+            "ms_per_ph_iteration": round(dt / max(args.uc_steps, 1) * 1000.0, 1),
+            "pdhg_steps_per_prox_qp": [round(v, 1) for v in steps],
+            "not_optimal_after": int((b.status != 0).sum().item()),
+            "parity": "unpinned (no reference file holds UC LP values); the oracle restatement matches "
+                      "the Iter0 bounds to 2e-9 (tests/test_gpu_parity.py::test_uc_lp_relaxation_matches_oracle)"}
+
+
 def _spawn_ranks(n, cpu):
     """`bench.py --gpus N` without a launcher: this parent (which has not
     touched the GPU) starts N rank processes, one per GPU, with the
@@ -560,7 +619,10 @@ def _parser():
     ap.add_argument("--f4-crops", type=int, default=1000)
     ap.add_argument("--sslp-scens", type=int, default=10000,
                     help="scenarios per rank of the sslp companion config (BASELINE config 5); 0 = skip")
-    ap.add_argument("--only", choices=["f3", "f4", "sslp"], default=None,
+    ap.add_argument("--uc-scens", type=int, default=4,
+                    help="scenarios per rank of the UC companion config (BASELINE config 4's model); 0 = skip")
+    ap.add_argument("--uc-steps", type=int, default=1, help="PH iterations of the UC companion")
+    ap.add_argument("--only", choices=["f3", "f4", "sslp", "uc"], default=None,
                     help="profiling: run ONLY this companion config, exactly as the full line runs "
                          "it (its timed window is then the last --hbm-steps solve calls of the "
                          "process, the window tools/pmc_summary.py reads); prints its JSON")
@@ -615,7 +677,8 @@ def run():
               "device_loop_graphs": False}
         res = {"f3": lambda: hbm_config(args, world, farmer, PH, o1),
                "f4": lambda: big_config(args, world, farmer, PH, o1),
-               "sslp": lambda: sslp_config(args, world, PH, o1)}[args.only]()
+               "sslp": lambda: sslp_config(args, world, PH, o1),
+               "uc": lambda: uc_config(args, world, PH, o1)}[args.only]()
         if world > 1:
             dist.destroy_process_group()
         return {"only": args.only, args.only: res} if rank == 0 else None
@@ -784,6 +847,11 @@ def run():
         _progress("companion config sslp")
         sslp = sslp_config(args, world, PH, opts)
 
+    ucc = None
+    if args.uc_scens > 0:
+        _progress("companion config UC")
+        ucc = uc_config(args, world, PH, opts)
+
     if rank == 0:
         value = S * args.steps / dt
         n, m, nnz = farmer_dims(c)
@@ -844,6 +912,7 @@ def run():
             "hbm_config": f3,
             "f4_config": f4,
             "sslp_config": sslp,
+            "uc_config": ucc,
         }
     else:
         out = None

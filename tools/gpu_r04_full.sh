@@ -1,0 +1,13 @@
+#!/bin/bash
+# The whole GPU suite, then smoke().
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+O=$R/gpurun_out
+mkdir -p $O
+cd $R
+export TMPDIR=/tmp
+timeout -k 10 1300 python -u -m pytest -v --timeout 600 --timeout-method thread -m gpu tests/ > $O/pytest_gpu_full.log 2>&1; rc=$?
+grep -E "PASSED|FAILED|ERROR|passed|failed" $O/pytest_gpu_full.log | tail -70
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -3 $O/smoke.log

@@ -43,5 +43,5 @@ if on f4; then
   python3 tools/pmc_summary.py $O/f4_fetch $O/f4_write $O/f4_stats $O/pmc_summary_f4_iter0.json farmer1k_c1000 first > /dev/null || { echo "pmc f4 iter0 summary failed"; exit 1; }
   cp $O/pmc_summary_f4_iter0.json profiles/$TAG/
 fi
-on f2 && { prof f2 20 farmer10k_c1 $NOCPU --hbm-crops 0 --sslp-scens 0 --f4-scens 0 || exit 1; }
+on f2 && { prof f2 20 farmer10k_c1 $NOCPU --hbm-crops 0 --sslp-scens 0 --f4-scens 0 --uc-scens 0 || exit 1; }
 echo ALLDONE

@@ -63,7 +63,8 @@ st = b.status.cpu().numpy()
 it = b.iters.cpu().numpy()
 d = b.diagnostics()
 say(f"Iter0 {dt:.2f} s: trivial bound {tb:.6f}, statuses {np.bincount(st, minlength=4)}, PDHG steps mean "
-    f"{it.mean():.0f} max {it.max()}, how {np.bincount(d[:, 4].astype(int), minlength=4)}")
+    f"{it.mean():.0f} max {it.max()}, how {np.bincount(d[:, 4].astype(int), minlength=4)}; per scenario "
+    f"{it.tolist()}")
 print("  final errors of the first scenarios:", d[:3, :3], flush=True)
 nt, _, _, _, nk, k_ms, np_, p_ms = b.read_timing_full()
 say(f"  big_kernel {nk} launches {k_ms:.1f} ms, polish {np_} launches {p_ms:.1f} ms; "
