@@ -1801,6 +1801,133 @@ __device__ __forceinline__ int as_eval(const SolveArgs &a, int s, int lane, cons
   return AS_HIT;
 }
 
+// Sum over this lane's 32-lane half (lanes 0-31 / 32-63), uniform within
+// the half: wave_sum's DPP steps stay inside 16-lane rows, then the half's
+// two row sums.  For data in lanes 0..31 of one half it adds exactly what
+// wave_sum adds for the same data in lanes 0..31 of a wave (the other two
+// row sums are zeros there), so a scenario's check is bitwise the same on
+// either half.
+__device__ __forceinline__ double half_sum(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  v += dpp_f64<0x140>(v);
+  const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16);
+  const double r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
+  return (threadIdx.x & 32) ? r2 + r3 : r0 + r1;
+}
+
+// as_eval for two scenarios on one wave (n, m <= 32): lanes 0-31 scenario
+// sA, lanes 32-63 scenario sB (sB < 0: none).  Every per-lane quantity is
+// as_eval's for lane `lane & 31` of the lane's own scenario (PH terms of
+// slot k in lane base + k); results per half (rA / rB, sigA / sigB, XN of
+// the lane's scenario).
+__device__ __forceinline__ void as_eval2(const SolveArgs &a, int sA, int sB, int lane, const double *entA,
+                                         const double *entB, const double *sbA, const double *sbB,
+                                         const double *vsA, const double *vsB, const Pattern &P, double *xsw,
+                                         int okA, int okB, double hk_l, double qk_l, double cst_l, int kslot,
+                                         double &XN_out, int &rA, int &rB, unsigned long long (&sigA)[4],
+                                         unsigned long long (&sigB)[4]) {
+  const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m);
+  const int hb = lane & 32, hl = lane & 31;
+  const bool hiB = hb != 0, live = hiB ? sB >= 0 : true;
+  const int s = hiB ? sB : sA;
+  const double *ent = hiB ? entB : entA, *sb = hiB ? sbB : sbA, *vs = hiB ? vsB : vsA;
+  const bool cn = live && hl < n, cm = live && hl < m;
+  const double *B = ent + K;
+  double DC = 1.0, G = 0.0, L = 0.0, U = 0.0, XU = 0.0, ATY = 0.0;
+  if (cn) {
+    G = sb[hl];
+    L = sb[n + hl];
+    U = sb[2 * n + hl];
+    DC = sb[3 * n + hl];
+    XU = B[cv_x(n, m) + hl];
+    ATY = B[cv_aty(n, m) + hl];
+  }
+  double DR = 1.0, RL = 0.0, RU = 0.0, YU = 0.0, AX = 0.0;
+  if (cm) {
+    RL = sb[4 * n + hl];
+    RU = sb[4 * n + m + hl];
+    DR = sb[4 * n + 2 * m + hl];
+    YU = B[cv_y(n, m) + hl];
+    AX = B[cv_ax(n, m) + hl];
+  }
+  const double key_l = (live && hl < K) ? ent[hl] : 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double hk = __shfl(hk_l, hb + k, WAVE);
+    const double *Dk = B + (size_t)(k + 1) * VL;
+    if (cn) {
+      XU = fma(hk, Dk[cv_x(n, m) + hl], XU);
+      ATY = fma(hk, Dk[cv_aty(n, m) + hl], ATY);
+    }
+    if (cm) {
+      YU = fma(hk, Dk[cv_y(n, m) + hl], YU);
+      AX = fma(hk, Dk[cv_ax(n, m) + hl], AX);
+    }
+  }
+  const int ks = kslot >= 0 ? kslot : 0;
+  const double hj = __shfl(hk_l, hb + ks, WAVE);
+  const double qj = __shfl(qk_l, hb + ks, WAVE);
+  const double keyj = __shfl(key_l, hb + ks, WAVE);
+  if (kslot >= 0) G += hj * DC;
+  const double Q = (kslot >= 0 ? qj : 0.0) * DC * DC;
+  const unsigned long long bad = __ballot(cn && kslot >= 0 && keyj != Q);
+  const bool noA = !okA || (bad & 0xffffffffull), noB = sB < 0 || !okB || (bad >> 32);
+  const bool no = hiB ? noB : noA;
+  double XN = cn ? clampd(XU, L, U) : 0.0;
+  const double YN = YU;
+  double AXN = AX;
+  const unsigned long long clip = __ballot(cn && !no && XN != XU);
+  if (clip) {
+    if (cn) xsw[lane] = XN;  // (each half its own 32 entries)
+    wsync();
+    const bool mine = hiB ? (clip >> 32) != 0 : (clip & 0xffffffffull) != 0;
+    double r = 0.0;
+    if (cm)
+      for (int p = P.row_ptr[hl]; p < P.row_ptr[hl + 1]; ++p) r = fma(vs[p], xsw[hb + P.col_idx[p]], r);
+    if (mine) AXN = r;
+  }
+  double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double lam = 0.0;
+  if (cn) kkt_terms_col(XN, G, Q, L, U, DC, ATY, lam, v);
+  if (cm) kkt_terms_row(AXN, YN, RL, RU, DR, v);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[i] = half_sum(v[i]);
+  const double cst = half_sum(live ? cst_l : 0.0);
+  double ep, ed, eg, pobj, dobj;
+  kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
+  const bool acc = !no && ep <= a.tol && ed <= a.tol && eg <= a.tol;
+  // the moved active sets' primal-dual active-set steps (per half)
+  const double lamu = Q * XU + G - ATY;
+  const ActiveSet as = classify_pdas(hl, cn ? n : 0, cm ? m : 0, XU, lamu, YU, AX, L, U, RL, RU);
+  unsigned long long sg[4];
+  as.signature(sg);
+  for (int i = 0; i < 4; ++i) {
+    sigA[i] = sg[i] & 0xffffffffull;
+    sigB[i] = sg[i] >> 32;
+  }
+  const unsigned long long am = __ballot(acc && hl == 0);
+  rA = noA ? AS_NOENTRY : ((am & 1ull) ? AS_HIT : AS_MOVED);
+  rB = noB ? AS_NOENTRY : ((am >> 32) & 1ull ? AS_HIT : AS_MOVED);
+  if (acc) {
+    if (cn) a.x[(size_t)hl * S + s] = XN * DC;
+    if (cm) a.y[(size_t)hl * S + s] = YN * DR;
+    if (hl == 0) {
+      a.status[s] = PH_STATUS_OPTIMAL;
+      a.iters[s] = 0;
+      a.pobj[s] = pobj;
+      a.dbound[s] = dobj;
+      double *dg = a.diag + PH_DIAG_W * (size_t)s;
+      dg[0] = ep;
+      dg[1] = ed;
+      dg[2] = eg;
+      dg[3] = -1.0;
+      dg[4] = 3.0;
+    }
+  }
+  XN_out = XN;
+}
+
 // One wave evaluates SPW consecutive scenarios: their entries and static
 // blocks are contiguous, so they stage in one round of coalesced loads.
 template <int WPB, int SPW>
@@ -2798,7 +2925,7 @@ struct LoopArgs {
   int32_t *ctr;                // the batch's counters (0: misses, 1, 2: tail list count, 6)
   double *part_x;              // [grid][2G+2] sums / misses / tails partials
   double *part_c;              // [grid] conv partials
-  int32_t *bar;                // [2] arrival counter, abort flag (zeroed before each launch)
+  int32_t *bar;                // [LBAR_WORDS] barrier words (grid_sync; zeroed before each launch)
   int spw;                     // scenario slots per wave
   unsigned long long *prof;    // phase clocks (ph_debug_prof slots 20-28) or null
 };
@@ -2872,22 +2999,34 @@ __device__ __forceinline__ void grid_combine(const double *part, int PQ, int Q, 
 // complete before its arrival (vmcnt), then thread 0 waits for every
 // block's arrival of this generation.  False on an abort (timeout here or
 // in another block).
+// Hierarchical (XCD-style) form: the blocks b = g mod 8 arrive on their
+// group's counter (one 64-B line each), the last of a group on the top
+// counter, the last group's last block writes the generation to the release
+// word every block polls (fan-ins of ~32 and 8 arrivals instead of 256 on
+// one word: MI355X_MICROARCH.md barrier-xcd, 4.1 against 7.4 us).  Words:
+// bar[16 g] group counters, bar[LBAR_TOP], bar[LBAR_REL], bar[LBAR_ABORT].
+constexpr int LBAR_TOP = 128, LBAR_REL = 144, LBAR_ABORT = 160, LBAR_WORDS = 176;
 __device__ __forceinline__ bool grid_sync(int32_t *bar, unsigned &gen, int *flag, int32_t *err) {
   __syncthreads();
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gen += 1u;
-    const int target = (int)(gen * gridDim.x);
-    __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int G = gridDim.x, g = blockIdx.x % 8, ng = (G - g + 7) / 8, ngroups = G < 8 ? G : 8;
+    const int a = __hip_atomic_fetch_add(bar + 16 * g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a == (int)gen * ng - 1) {  // the group's last arrival
+      const int t = __hip_atomic_fetch_add(bar + LBAR_TOP, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == (int)gen * ngroups - 1)
+        __hip_atomic_store(bar + LBAR_REL, (int)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     int ok = 1;
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    while (__hip_atomic_load(bar + LBAR_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int)gen) {
+      if (__hip_atomic_load(bar + LBAR_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ok = 0;
         break;
       }
       if (wall_clock64() - t0 > LOOP_BAR_TICKS) {
-        __hip_atomic_store(bar + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(bar + LBAR_ABORT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         dev_fail(err, CHK_BARRIER, (int)gen, (int)blockIdx.x);
         ok = 0;
         break;
@@ -2966,6 +3105,7 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
     }
   }
   const int kslot = lane < n ? a.slot_of_col[lane] : -1;
+  const int kslot2 = (lane & 31) < n ? a.slot_of_col[lane & 31] : -1;  // (as_eval2: per half)
   const int jk = lane < K ? a.nonant_col[lane] : 0;
   unsigned gen = 0;
   bool ok = ran, aborted = false;
@@ -3036,57 +3176,76 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
     for (int q = lane; q < 2 * G; q += WAVE) ACC[q] = 0.0;
     int nmiss = 0, ntail = 0, npol = 0;
     wsync();
-    for (int j = 0; j < ns; ++j) {
-      const int s = s0 + j;
-      double hk_l, qk_l, cst_l;
-      ph_lane_terms(a, lane, lane < K ? WW[j * K + lane] : 0.0, lane < K ? RHO[j * K + lane] : 0.0,
-                    lane < K ? XBV[j * K + lane] : 0.0, hk_l, qk_l, cst_l);
-      const double *ent_j = ENT + (size_t)j * CW, *sb_j = SBV + (size_t)j * SBW, *vl_j = VLV + (size_t)j * nnz;
-      double XN = 0.0;
-      unsigned long long sig[4];
-      const int r = as_eval(a, s, lane, ent_j, sb_j, vl_j, Pl, ws.xs, OKV[j], hk_l, qk_l, cst_l, kslot,
-                            XN, sig);
-      bool solved = r == AS_HIT;
-      if (!solved) {
-        ++nmiss;
-        if (r == AS_MOVED) {
-          if (lane < 4) a.hint[4 * (size_t)s + lane] = sig[lane];
-          if (lane == 0) a.hint_ok[s] = 1;
+    // two owned scenarios per wave at a time (lanes 0-31 / 32-63: as_eval2,
+    // n, m <= 32), a miss then polished by the whole wave
+    const int hb = lane & 32, hl = lane & 31;
+    for (int j = 0; j < ns; j += 2) {
+      const int jB = j + 1 < ns ? j + 1 : -1;
+      const int jh = (hb && jB >= 0) ? jB : j;  // this lane's scenario
+      double hk2, qk2, cst2;
+      ph_lane_terms(a, hl, hl < K ? WW[jh * K + hl] : 0.0, hl < K ? RHO[jh * K + hl] : 0.0,
+                    hl < K ? XBV[jh * K + hl] : 0.0, hk2, qk2, cst2);
+      const int jb2 = jB >= 0 ? jB : j;
+      double XN2 = 0.0;
+      int rr[2];
+      unsigned long long sg[2][4];
+      as_eval2(a, s0 + j, jB >= 0 ? s0 + jB : -1, lane, ENT + (size_t)j * CW, ENT + (size_t)jb2 * CW,
+               SBV + (size_t)j * SBW, SBV + (size_t)jb2 * SBW, VLV + (size_t)j * nnz, VLV + (size_t)jb2 * nnz,
+               Pl, ws.xs, OKV[j], jB >= 0 ? OKV[jB] : 0, hk2, qk2, cst2, kslot2, XN2, rr[0], rr[1], sg[0], sg[1]);
+      for (int u = 0; u < 2; ++u) {
+        const int jc = u ? jB : j;
+        if (jc < 0) break;
+        const int s = s0 + jc;
+        const double *sb_j = SBV + (size_t)jc * SBW, *vl_j = VLV + (size_t)jc * nnz;
+        bool solved = rr[u] == AS_HIT;
+        double xj = 0.0;
+        if (solved) {  // nonant k's value from the half that checked it
+          const double dc = lane < K ? sb_j[3 * n + jk] : 1.0;
+          xj = __shfl(XN2, (u ? 32 : 0) + jk, WAVE) * dc;
         } else {
-          for (int i = 0; i < 4; ++i) sig[i] = a.hint[4 * (size_t)s + i];
-        }
-        wsync();
-        const unsigned long long tp0 = L.prof ? wall_clock64() : 0ull;
-        solved = polish_one(a, s, lane, ws, pt, vl_j, sb_j, hk_l, qk_l, cst_l, kslot, sig,
-                            ENT + (size_t)j * CW, XN);
-        if (L.prof) {
-          tpol += wall_clock64() - tp0;
-          ++npolw;
-        }
-        if (solved) {
-          ++npol;
-          if (lane == 0) OKV[j] = 1;
-        } else {
-          ++ntail;
-          if (lane == 0) {
-            a.hint_ok[s] = 0;
-            list_push(a.wl2, a.wl2_count, s, S, a.err);
+          ++nmiss;
+          double hk_l, qk_l, cst_l;
+          ph_lane_terms(a, lane, lane < K ? WW[jc * K + lane] : 0.0, lane < K ? RHO[jc * K + lane] : 0.0,
+                        lane < K ? XBV[jc * K + lane] : 0.0, hk_l, qk_l, cst_l);
+          unsigned long long sig[4];
+          if (rr[u] == AS_MOVED) {
+            for (int i = 0; i < 4; ++i) sig[i] = sg[u][i];
+            if (lane < 4) a.hint[4 * (size_t)s + lane] = sig[lane];
+            if (lane == 0) a.hint_ok[s] = 1;
+          } else {
+            for (int i = 0; i < 4; ++i) sig[i] = a.hint[4 * (size_t)s + i];
+          }
+          wsync();
+          const unsigned long long tp0 = L.prof ? wall_clock64() : 0ull;
+          double XN = 0.0;
+          solved = polish_one(a, s, lane, ws, pt, vl_j, sb_j, hk_l, qk_l, cst_l, kslot, sig,
+                              ENT + (size_t)jc * CW, XN);
+          if (L.prof) {
+            tpol += wall_clock64() - tp0;
+            ++npolw;
+          }
+          if (solved) {
+            ++npol;
+            if (lane == 0) OKV[jc] = 1;
+            const double dcj = __shfl(lane < n ? sb_j[3 * n + lane] : 1.0, jk, WAVE);
+            xj = __shfl(XN, jk, WAVE) * dcj;
+          } else {
+            ++ntail;
+            if (lane == 0) {
+              a.hint_ok[s] = 0;
+              list_push(a.wl2, a.wl2_count, s, S, a.err);
+            }
           }
         }
-      }
-      if (solved) {
-        // this scenario's nonant values and Compute_Xbar terms
-        const double dcj = __shfl(lane < n ? sb_j[3 * n + lane] : 1.0, jk, WAVE);
-        const double xj = __shfl(XN, jk, WAVE) * dcj;
-        if (lane < K) {
-          XNV[j * K + lane] = xj;
-          const int g = GID[j * K + lane];
-          const double p = PCV[j * K + lane];
+        if (solved && lane < K) {  // this scenario's nonant values and Compute_Xbar terms
+          XNV[jc * K + lane] = xj;
+          const int g = GID[jc * K + lane];
+          const double p = PCV[jc * K + lane];
           ACC[g] += p * xj;
           ACC[G + g] += p * xj * xj;
         }
+        wsync();
       }
-      wsync();
     }
     if (lane == 0) {
       ACC[2 * G] = (double)nmiss;
@@ -3265,7 +3424,7 @@ struct ph_batch {
   int loop_grid = 0, loop_spw = 0, loop_G = 0;  // resident blocks, scenario slots per wave, for G
   size_t loop_lds_bytes = 0;
   double *d_lpart = nullptr;    // [grid][2G+2] + [grid] partials
-  int32_t *d_lbar = nullptr;    // [2] barrier counter, abort flag
+  int32_t *d_lbar = nullptr;    // [LBAR_WORDS] loop_kernel barrier words
 };
 
 namespace {
@@ -4418,12 +4577,10 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     hipLaunchKernelGGL(polish_kernel, dim3(std::min(b->S, POLISH_GRID)), dim3(WAVE),
                        polish_lds_bytes(b), b->stream, a);
     HIP_OK(hipGetLastError());
+    if (tev) HIP_OK(hipEventRecord(tev[2], b->stream));  // (polish | tail: separate times)
     a.ul = nullptr;  // (the tail bounds its failures itself)
     if (int rc = launch_tail(b, a, lds)) return rc;
-    if (tev) {
-      HIP_OK(hipEventRecord(tev[2], b->stream));
-      HIP_OK(hipEventRecord(tev[3], b->stream));
-    }
+    if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
   } else {
     if (tev) {
       HIP_OK(hipEventRecord(tev[1], b->stream));
@@ -4719,7 +4876,7 @@ static int loop_persist_setup(ph_batch *b, bool *ok) {
   const bool env_on = env && std::atoi(env) != 0;
   const ph_loop_pass_args &p = b->pass;
   if (!env_on || p.conv_part || b->mid || !polish_fits(b) || !b->d_sb || !b->d_cache || !p.opts.polish ||
-      !p.opts.warm_start || b->K <= 0 || b->K > RG_K || b->n > WAVE || b->m > WAVE || p.G <= 0 ||
+      !p.opts.warm_start || b->K <= 0 || b->K > RG_K || b->n > WAVE / 2 || b->m > WAVE / 2 || p.G <= 0 ||
       p.G > 512 || b->loop_xa.G != p.G || b->loop_xa.C <= 0 || b->loop_xa.x != p.x ||
       b->loop_xa.out != p.sums)
     return PH_OK;
@@ -4741,7 +4898,7 @@ static int loop_persist_setup(ph_batch *b, bool *ok) {
     b->d_lpart = nullptr;
     if (int rc = dalloc(&b->d_lpart, (size_t)NB * (2 * p.G + 3))) return rc;
     if (!b->d_lbar)
-      if (int rc = dalloc(&b->d_lbar, 2)) return rc;
+      if (int rc = dalloc(&b->d_lbar, LBAR_WORDS)) return rc;
     b->loop_grid = NB;  // <= CUs x per_cu: every block resident
     b->loop_spw = spw;
     b->loop_G = p.G;
@@ -4751,10 +4908,9 @@ static int loop_persist_setup(ph_batch *b, bool *ok) {
   return PH_OK;
 }
 
-__global__ void loop_prep_kernel(LoopCtl *c, int32_t *bar, int iters, int first) {
-  bar[0] = 0;
-  bar[1] = 0;
-  if (first) c->iter_end = c->iter + iters;
+__global__ void __launch_bounds__(WAVE) loop_prep_kernel(LoopCtl *c, int32_t *bar, int iters, int first) {
+  for (int q = threadIdx.x; q < LBAR_WORDS; q += WAVE) bar[q] = 0;
+  if (first && threadIdx.x == 0) c->iter_end = c->iter + iters;
 }
 
 int ph_loop_persistent(ph_batch_t b) {
@@ -4832,7 +4988,7 @@ int ph_loop_run(ph_batch_t b, int32_t iters) {
   constexpr int ROUNDS = 4;
   const int post_g = b->loop_xa.G * std::max(1, b->loop_xa.C);
   for (int r = 0; r < ROUNDS; ++r) {
-    hipLaunchKernelGGL(loop_prep_kernel, dim3(1), dim3(1), 0, b->stream, b->d_ctl, b->d_lbar, (int)iters,
+    hipLaunchKernelGGL(loop_prep_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_ctl, b->d_lbar, (int)iters,
                        r == 0 ? 1 : 0);
     if (int rc = phase_event(b, 2)) return rc;
     hipLaunchKernelGGL(loop_kernel, dim3(b->loop_grid), dim3(LOOP_WPB * WAVE), b->loop_lds_bytes, b->stream, L);
