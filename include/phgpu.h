@@ -337,9 +337,10 @@ int ph_loop_pass(ph_batch_t b);
 /*
  * Up to `iters` passes of the bound loop in one call, same results as that
  * many ph_loop_pass calls (up to the summation order of Compute_Xbar's sums
- * and of conv).  With PHGPU_PERSIST=1 (opt-in: at F2 it measured no faster
- * than the per-pass kernels), one rank and the one-wave cached warm solve: a
- * persistent launch runs whole passes with two grid barriers each (Compute_Xbar
+ * and of conv).  With one rank and the one-wave cached warm solve, once
+ * ph_loop_status has seen a quiet stretch (no PDHG tail, at most 2e-3 cache
+ * misses per scenario-pass since its previous read; PHGPU_PERSIST=1 / 0
+ * forces the choice): a persistent launch runs whole passes with two grid barriers each (Compute_Xbar
  * broadcast + Update_W + conv, then the cached map / register polish of every
  * scenario and the next sums) while the owned scenarios' data stay in LDS;
  * a pass with a polish failure is finished by the tail and post-solve

@@ -1801,38 +1801,48 @@ __device__ __forceinline__ int as_eval(const SolveArgs &a, int s, int lane, cons
   return AS_HIT;
 }
 
-// Sum over this lane's 32-lane half (lanes 0-31 / 32-63), uniform within
-// the half: wave_sum's DPP steps stay inside 16-lane rows, then the half's
-// two row sums.  For data in lanes 0..31 of one half it adds exactly what
-// wave_sum adds for the same data in lanes 0..31 of a wave (the other two
-// row sums are zeros there), so a scenario's check is bitwise the same on
-// either half.
-__device__ __forceinline__ double half_sum(double v) {
+// Sum over this lane's group of LPS lanes (16: one DPP row, 32: a half
+// wave), uniform within the group.  The DPP steps stay inside 16-lane rows
+// (after them every lane holds its row's sum); a 32-lane group adds its two
+// row sums.  For a scenario's data in its group's first lanes this adds
+// exactly what wave_sum adds for the same data in lanes 0.. of a wave (the
+// other row sums are zeros there), so the check is bitwise as_eval's.
+template <int LPS>
+__device__ __forceinline__ double group_sum(double v) {
   v += dpp_f64<0xB1>(v);
   v += dpp_f64<0x4E>(v);
   v += dpp_f64<0x141>(v);
   v += dpp_f64<0x140>(v);
-  const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16);
-  const double r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
-  return (threadIdx.x & 32) ? r2 + r3 : r0 + r1;
+  if constexpr (LPS == 16) {
+    return v;
+  } else {
+    const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16);
+    const double r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
+    return (threadIdx.x & 32) ? r2 + r3 : r0 + r1;
+  }
 }
 
-// as_eval for two scenarios on one wave (n, m <= 32): lanes 0-31 scenario
-// sA, lanes 32-63 scenario sB (sB < 0: none).  Every per-lane quantity is
-// as_eval's for lane `lane & 31` of the lane's own scenario (PH terms of
-// slot k in lane base + k); results per half (rA / rB, sigA / sigB, XN of
-// the lane's scenario).
-__device__ __forceinline__ void as_eval2(const SolveArgs &a, int sA, int sB, int lane, const double *entA,
-                                         const double *entB, const double *sbA, const double *sbB,
-                                         const double *vsA, const double *vsB, const Pattern &P, double *xsw,
-                                         int okA, int okB, double hk_l, double qk_l, double cst_l, int kslot,
-                                         double &XN_out, int &rA, int &rB, unsigned long long (&sigA)[4],
-                                         unsigned long long (&sigB)[4]) {
-  const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m);
-  const int hb = lane & 32, hl = lane & 31;
-  const bool hiB = hb != 0, live = hiB ? sB >= 0 : true;
-  const int s = hiB ? sB : sA;
-  const double *ent = hiB ? entB : entA, *sb = hiB ? sbB : sbA, *vs = hiB ? vsB : vsA;
+// as_eval for 64 / LPS scenarios on one wave (n, m <= LPS): lanes g*LPS ..
+// of group g check the resident scenario slot jg[g] (< 0: none) of the
+// wave's arrays (ENT / SBV / VLV / OKV, scenario s0 + slot).  Every per-lane
+// quantity is as_eval's for lane `lane % LPS` of the lane's own scenario
+// (PH terms of slot k in lane g*LPS + k, kslot of column lane % LPS);
+// results per group: r[g], sig[g] (bits by column / row), XN per lane.
+template <int LPS>
+__device__ __forceinline__ void as_evalg(const SolveArgs &a, int s0, const int (&jg)[64 / LPS], int lane,
+                                         const double *ENT, const double *SBV, const double *VLV,
+                                         const int32_t *OKV, const Pattern &P, double *xsw, double hk_l,
+                                         double qk_l, double cst_l, int kslot, double &XN_out,
+                                         int (&r)[64 / LPS], unsigned long long (&sig)[64 / LPS][4]) {
+  constexpr int NG = 64 / LPS;
+  constexpr unsigned long long GM = LPS == 32 ? 0xffffffffull : 0xffffull;
+  const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m), CW = a.CW, SBW = 4 * n + 3 * m;
+  const int g = lane / LPS, gb = g * LPS, hl = lane % LPS;
+  const int j = jg[g];
+  const bool live = j >= 0;
+  const int s = s0 + (live ? j : 0);
+  const double *ent = ENT + (size_t)(live ? j : 0) * CW, *sb = SBV + (size_t)(live ? j : 0) * SBW;
+  const double *vs = VLV + (size_t)(live ? j : 0) * a.nnz;
   const bool cn = live && hl < n, cm = live && hl < m;
   const double *B = ent + K;
   double DC = 1.0, G = 0.0, L = 0.0, U = 0.0, XU = 0.0, ATY = 0.0;
@@ -1854,7 +1864,7 @@ __device__ __forceinline__ void as_eval2(const SolveArgs &a, int sA, int sB, int
   }
   const double key_l = (live && hl < K) ? ent[hl] : 0.0;
   for (int k = 0; k < K; ++k) {
-    const double hk = __shfl(hk_l, hb + k, WAVE);
+    const double hk = __shfl(hk_l, gb + k, WAVE);
     const double *Dk = B + (size_t)(k + 1) * VL;
     if (cn) {
       XU = fma(hk, Dk[cv_x(n, m) + hl], XU);
@@ -1866,49 +1876,51 @@ __device__ __forceinline__ void as_eval2(const SolveArgs &a, int sA, int sB, int
     }
   }
   const int ks = kslot >= 0 ? kslot : 0;
-  const double hj = __shfl(hk_l, hb + ks, WAVE);
-  const double qj = __shfl(qk_l, hb + ks, WAVE);
-  const double keyj = __shfl(key_l, hb + ks, WAVE);
+  const double hj = __shfl(hk_l, gb + ks, WAVE);
+  const double qj = __shfl(qk_l, gb + ks, WAVE);
+  const double keyj = __shfl(key_l, gb + ks, WAVE);
   if (kslot >= 0) G += hj * DC;
   const double Q = (kslot >= 0 ? qj : 0.0) * DC * DC;
   const unsigned long long bad = __ballot(cn && kslot >= 0 && keyj != Q);
-  const bool noA = !okA || (bad & 0xffffffffull), noB = sB < 0 || !okB || (bad >> 32);
-  const bool no = hiB ? noB : noA;
+  bool nog[NG];
+#pragma unroll
+  for (int q = 0; q < NG; ++q) nog[q] = jg[q] < 0 || !OKV[jg[q] < 0 ? 0 : jg[q]] || ((bad >> (q * LPS)) & GM);
+  const bool no = nog[g];
   double XN = cn ? clampd(XU, L, U) : 0.0;
   const double YN = YU;
   double AXN = AX;
   const unsigned long long clip = __ballot(cn && !no && XN != XU);
   if (clip) {
-    if (cn) xsw[lane] = XN;  // (each half its own 32 entries)
+    if (cn) xsw[lane] = XN;  // (each group its own LPS entries)
     wsync();
-    const bool mine = hiB ? (clip >> 32) != 0 : (clip & 0xffffffffull) != 0;
-    double r = 0.0;
+    const bool mine = ((clip >> gb) & GM) != 0;
+    double rr = 0.0;
     if (cm)
-      for (int p = P.row_ptr[hl]; p < P.row_ptr[hl + 1]; ++p) r = fma(vs[p], xsw[hb + P.col_idx[p]], r);
-    if (mine) AXN = r;
+      for (int p = P.row_ptr[hl]; p < P.row_ptr[hl + 1]; ++p) rr = fma(vs[p], xsw[gb + P.col_idx[p]], rr);
+    if (mine) AXN = rr;
   }
   double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   double lam = 0.0;
   if (cn) kkt_terms_col(XN, G, Q, L, U, DC, ATY, lam, v);
   if (cm) kkt_terms_row(AXN, YN, RL, RU, DR, v);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) v[i] = half_sum(v[i]);
-  const double cst = half_sum(live ? cst_l : 0.0);
+  for (int i = 0; i < 6; ++i) v[i] = group_sum<LPS>(v[i]);
+  const double cst = group_sum<LPS>(live ? cst_l : 0.0);
   double ep, ed, eg, pobj, dobj;
   kkt_rel(v, cst, ep, ed, eg, pobj, dobj);
   const bool acc = !no && ep <= a.tol && ed <= a.tol && eg <= a.tol;
-  // the moved active sets' primal-dual active-set steps (per half)
+  // the moved active sets' primal-dual active-set steps (per group)
   const double lamu = Q * XU + G - ATY;
   const ActiveSet as = classify_pdas(hl, cn ? n : 0, cm ? m : 0, XU, lamu, YU, AX, L, U, RL, RU);
   unsigned long long sg[4];
   as.signature(sg);
-  for (int i = 0; i < 4; ++i) {
-    sigA[i] = sg[i] & 0xffffffffull;
-    sigB[i] = sg[i] >> 32;
-  }
   const unsigned long long am = __ballot(acc && hl == 0);
-  rA = noA ? AS_NOENTRY : ((am & 1ull) ? AS_HIT : AS_MOVED);
-  rB = noB ? AS_NOENTRY : ((am >> 32) & 1ull ? AS_HIT : AS_MOVED);
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sig[q][i] = (sg[i] >> (q * LPS)) & GM;
+    r[q] = nog[q] ? AS_NOENTRY : (((am >> (q * LPS)) & 1ull) ? AS_HIT : AS_MOVED);
+  }
   if (acc) {
     if (cn) a.x[(size_t)hl * S + s] = XN * DC;
     if (cm) a.y[(size_t)hl * S + s] = YN * DR;
@@ -3039,6 +3051,9 @@ __device__ __forceinline__ bool grid_sync(int32_t *bar, unsigned &gen, int *flag
   return *(volatile int *)flag != 0;
 }
 
+// LPS: lanes per scenario in the cached-map check (as_evalg; 16 when n, m
+// <= 16: four scenarios per wave, else 32: two)
+template <int LPS>
 __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const SolveArgs &a = L.a;
@@ -3105,7 +3120,7 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
     }
   }
   const int kslot = lane < n ? a.slot_of_col[lane] : -1;
-  const int kslot2 = (lane & 31) < n ? a.slot_of_col[lane & 31] : -1;  // (as_eval2: per half)
+  const int kslotg = (lane % LPS) < n ? a.slot_of_col[lane % LPS] : -1;  // (as_evalg: per group)
   const int jk = lane < K ? a.nonant_col[lane] : 0;
   unsigned gen = 0;
   bool ok = ran, aborted = false;
@@ -3176,24 +3191,24 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
     for (int q = lane; q < 2 * G; q += WAVE) ACC[q] = 0.0;
     int nmiss = 0, ntail = 0, npol = 0;
     wsync();
-    // two owned scenarios per wave at a time (lanes 0-31 / 32-63: as_eval2,
-    // n, m <= 32), a miss then polished by the whole wave
-    const int hb = lane & 32, hl = lane & 31;
-    for (int j = 0; j < ns; j += 2) {
-      const int jB = j + 1 < ns ? j + 1 : -1;
-      const int jh = (hb && jB >= 0) ? jB : j;  // this lane's scenario
+    // 64 / LPS owned scenarios per wave at a time (as_evalg, one group of
+    // LPS lanes each), a miss then polished by the whole wave
+    constexpr int NG = 64 / LPS;
+    const int gg = lane / LPS, gl = lane % LPS;
+    for (int j = 0; j < ns; j += NG) {
+      int jg[NG];
+#pragma unroll
+      for (int q = 0; q < NG; ++q) jg[q] = j + q < ns ? j + q : -1;
+      const int jh = jg[gg] >= 0 ? jg[gg] : j;  // this lane's scenario
       double hk2, qk2, cst2;
-      ph_lane_terms(a, hl, hl < K ? WW[jh * K + hl] : 0.0, hl < K ? RHO[jh * K + hl] : 0.0,
-                    hl < K ? XBV[jh * K + hl] : 0.0, hk2, qk2, cst2);
-      const int jb2 = jB >= 0 ? jB : j;
+      ph_lane_terms(a, gl, gl < K ? WW[jh * K + gl] : 0.0, gl < K ? RHO[jh * K + gl] : 0.0,
+                    gl < K ? XBV[jh * K + gl] : 0.0, hk2, qk2, cst2);
       double XN2 = 0.0;
-      int rr[2];
-      unsigned long long sg[2][4];
-      as_eval2(a, s0 + j, jB >= 0 ? s0 + jB : -1, lane, ENT + (size_t)j * CW, ENT + (size_t)jb2 * CW,
-               SBV + (size_t)j * SBW, SBV + (size_t)jb2 * SBW, VLV + (size_t)j * nnz, VLV + (size_t)jb2 * nnz,
-               Pl, ws.xs, OKV[j], jB >= 0 ? OKV[jB] : 0, hk2, qk2, cst2, kslot2, XN2, rr[0], rr[1], sg[0], sg[1]);
-      for (int u = 0; u < 2; ++u) {
-        const int jc = u ? jB : j;
+      int rr[NG];
+      unsigned long long sg[NG][4];
+      as_evalg<LPS>(a, s0, jg, lane, ENT, SBV, VLV, OKV, Pl, ws.xs, hk2, qk2, cst2, kslotg, XN2, rr, sg);
+      for (int u = 0; u < NG; ++u) {
+        const int jc = jg[u];
         if (jc < 0) break;
         const int s = s0 + jc;
         const double *sb_j = SBV + (size_t)jc * SBW, *vl_j = VLV + (size_t)jc * nnz;
@@ -3201,7 +3216,7 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
         double xj = 0.0;
         if (solved) {  // nonant k's value from the half that checked it
           const double dc = lane < K ? sb_j[3 * n + jk] : 1.0;
-          xj = __shfl(XN2, (u ? 32 : 0) + jk, WAVE) * dc;
+          xj = __shfl(XN2, u * LPS + jk, WAVE) * dc;
         } else {
           ++nmiss;
           double hk_l, qk_l, cst_l;
@@ -3423,6 +3438,12 @@ struct ph_batch {
   // persistent device loop (ph_loop_run, loop_kernel)
   int loop_grid = 0, loop_spw = 0, loop_G = 0;  // resident blocks, scenario slots per wave, for G
   size_t loop_lds_bytes = 0;
+  // ph_loop_status's view of the recent passes (ph_loop_run's path choice):
+  // the counters at the last read, and over the passes between the last two
+  // reads the cache misses per scenario-pass and whether a tail ran
+  unsigned long long st_sp = 0, st_pol = 0, st_hit = 0;
+  double obs_miss = -1.0;
+  bool obs_tail = true;
   double *d_lpart = nullptr;    // [grid][2G+2] + [grid] partials
   int32_t *d_lbar = nullptr;    // [LBAR_WORDS] loop_kernel barrier words
 };
@@ -4689,6 +4710,7 @@ int ph_loop_reset(ph_batch_t b, int32_t start_iter, int32_t iter_limit, double c
   else h.iter += 1;
   HIP_OK(hipMemcpyAsync(b->d_ctl, &h, sizeof(h), hipMemcpyHostToDevice, b->stream));
   HIP_OK(hipStreamSynchronize(b->stream));  // h is on this stack frame
+  b->st_sp = b->st_pol = b->st_hit = 0;  // the counters restart (obs_* carry over)
   return PH_OK;
 }
 
@@ -4865,15 +4887,23 @@ int ph_loop_pass(ph_batch_t b) {
 // to this pass, and the owned scenarios' data fit one block's LDS on a
 // resident grid (PHGPU_PERSIST=1: on, measurement hook).  Sets up the grid,
 // the LDS size and the partial buffers on first use.
+constexpr double LOOP_MISS_RATE = 2e-3;
+
 static int loop_persist_setup(ph_batch *b, bool *ok) {
   *ok = false;
-  // opt-in (PHGPU_PERSIST=1, read per call: tests compare both paths).  At F2
-  // it measured no faster than the per-pass kernels (51.0 against 51.2 us per
-  // pass): two grid barriers cost 7.7 + ~10 us on the 8-XCD part and the
-  // solve phase runs one wave per SIMD (the polish's register budget), 2.4 us
-  // per owned scenario (tools/loop_prof.py, profiles/r04/loop_prof_f2.txt)
+  // PHGPU_PERSIST=1 / 0 forces the path (read per call: tests compare both);
+  // by default the persistent launch runs once ph_loop_status has seen a
+  // quiet stretch: no tail and at most LOOP_MISS_RATE cache misses per
+  // scenario-pass.  A tail ends the launch (its PDHG solve runs in
+  // tail_kernel) and the next launch reloads every owned scenario into LDS,
+  // and a wave polishes its own misses in turn, so the early, busy passes
+  // run faster as per-pass kernels (F2 passes 6..25: 0.061 against 0.074 ms
+  // per pass) and the quiet ones persistent (F2 late passes: 32.3 against
+  // 51.5 us; PH to 1e-4: 0.250 against 0.279 s, tools/loop_prof.py,
+  // profiles/r04/loop_prof_f2_quad.txt)
   const char *env = std::getenv("PHGPU_PERSIST");
-  const bool env_on = env && std::atoi(env) != 0;
+  const bool quiet = !b->obs_tail && b->obs_miss >= 0.0 && b->obs_miss <= LOOP_MISS_RATE;
+  const bool env_on = env && *env ? std::atoi(env) != 0 : quiet;
   const ph_loop_pass_args &p = b->pass;
   if (!env_on || p.conv_part || b->mid || !polish_fits(b) || !b->d_sb || !b->d_cache || !p.opts.polish ||
       !p.opts.warm_start || b->K <= 0 || b->K > RG_K || b->n > WAVE / 2 || b->m > WAVE / 2 || p.G <= 0 ||
@@ -4890,9 +4920,11 @@ static int loop_persist_setup(ph_batch *b, bool *ok) {
     const LoopLds lay = loop_lds(b->n, b->m, b->nnz, b->K, p.G, b->CW, spw);
     const size_t bytes = sizeof(double) * (size_t)lay.total;
     if (bytes > 160 * 1024) return PH_OK;
-    HIP_OK(hipFuncSetAttribute((const void *)loop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)bytes));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, loop_kernel, LOOP_WPB * WAVE, bytes));
+    const bool q16 = b->n <= 16 && b->m <= 16;
+    const void *kf = q16 ? (const void *)loop_kernel<16> : (const void *)loop_kernel<32>;
+    HIP_OK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    if (q16) HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, loop_kernel<16>, LOOP_WPB * WAVE, bytes));
+    else HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, loop_kernel<32>, LOOP_WPB * WAVE, bytes));
     if (per_cu < 1) return PH_OK;  // cannot be resident: the per-pass kernels
     if (b->d_lpart) HIP_OK(hipFree(b->d_lpart));
     b->d_lpart = nullptr;
@@ -4991,7 +5023,10 @@ int ph_loop_run(ph_batch_t b, int32_t iters) {
     hipLaunchKernelGGL(loop_prep_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_ctl, b->d_lbar, (int)iters,
                        r == 0 ? 1 : 0);
     if (int rc = phase_event(b, 2)) return rc;
-    hipLaunchKernelGGL(loop_kernel, dim3(b->loop_grid), dim3(LOOP_WPB * WAVE), b->loop_lds_bytes, b->stream, L);
+    if (b->n <= 16 && b->m <= 16)
+      hipLaunchKernelGGL(loop_kernel<16>, dim3(b->loop_grid), dim3(LOOP_WPB * WAVE), b->loop_lds_bytes, b->stream, L);
+    else
+      hipLaunchKernelGGL(loop_kernel<32>, dim3(b->loop_grid), dim3(LOOP_WPB * WAVE), b->loop_lds_bytes, b->stream, L);
     HIP_OK(hipGetLastError());
     if (int rc = phase_event(b, -1)) return rc;
     if (int rc = launch_tail(b, a, lds)) return rc;
@@ -5019,6 +5054,15 @@ int ph_loop_status(ph_batch_t b, int64_t *out) {
   out[5] = (int64_t)h.acc[3];
   out[6] = (int64_t)h.acc[4];
   out[7] = (int64_t)h.acc[5];
+  if (h.acc[1] > b->st_sp) {  // passes ran since the last read
+    const unsigned long long dsp = h.acc[1] - b->st_sp, dpol = h.acc[4] - b->st_pol,
+                             dhit = h.acc[5] - b->st_hit;
+    b->obs_miss = (double)dpol / (double)dsp;
+    b->obs_tail = dpol + dhit < dsp;  // some scenario needed a PDHG solve
+  }
+  b->st_sp = h.acc[1];
+  b->st_pol = h.acc[4];
+  b->st_hit = h.acc[5];
   return PH_OK;
 }
 

@@ -998,8 +998,11 @@ def test_persistent_loop_matches_per_pass_kernels(model, S, limit, auto, monkeyp
     if auto:
         assert p[1] == 1 and p[0] == k + 1
     assert np.allclose(p[2], q[2], rtol=1e-8, atol=1e-12)
+    # x-bar, W, x: the two paths sum Compute_Xbar in different orders, and
+    # the solves' 1e-9 KKT stop amplifies that over the iterations (as in
+    # test_host_loop_device_loop_and_graphs_agree: W to 5e-8)
     for a, b_ in zip(p[3:6], q[3:6]):
-        assert _rel(a, b_) < 1e-8
+        assert _rel(a, b_) < 5e-8
 
 
 def test_uc_lp_relaxation_matches_oracle():
