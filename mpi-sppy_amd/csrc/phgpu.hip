@@ -4216,6 +4216,13 @@ static int mid_init(ph_batch *b) {
     b->mid_grid = std::min(b->mid_grid, cap);
     b->mid_pgrid = std::min(b->mid_pgrid, cap);
   }
+  if (const char *v = std::getenv("PHGPU_VERBOSE"); v && std::atoi(v) != 0)
+    std::fprintf(stderr,
+                 "phgpu mid: n %d m %d nnz %d; KKT N %d nnzL %d levels %d (chain from %d) contributions %ld; "
+                 "PDHG LDS %zu B %d/CU grid %d; polish LDS %zu B %d/CU grid %d; workspace %s (%ld doubles)\n",
+                 b->n, b->m, b->nnz, b->md.k16.N, b->md.k16.nnzL, b->md.k16.NL, b->md.k16.chain0,
+                 (long)b->sym.ncontrib, b->mid_lds_bytes, per_cu, b->mid_grid, b->mid_plds_bytes, per_cu_p,
+                 b->mid_pgrid, b->md.ws_stride > 0 ? "HBM" : "LDS", (long)b->md.ws_stride);
   // the HBM polish workspace: one slice per block of every launch that runs
   // the polish (mid_polish_kernel; on one-wave batches rescue_kernel and
   // tail_kernel), not one per scenario

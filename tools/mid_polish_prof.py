@@ -1,7 +1,7 @@
 """GPU diagnostic: phase clocks of the mid-size LDL' polish (ph_debug_prof
 slots 9-15) over PH iterations of farmer S / c (eager device loop).
 
-    python tools/mid_polish_prof.py S C START NIT
+    python tools/mid_polish_prof.py S C START NIT      (C = 0: sslp_15_45 synthetic)
 """
 import ctypes
 import os
@@ -12,14 +12,19 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-sppy_amd"))
 import mpisppy_amd
 mpisppy_amd.disable_tictoc_output()
 from mpisppy_amd.opt.ph import PH
-from mpisppy_amd.examples import farmer
+from mpisppy_amd.examples import farmer, sslp
 
 S, C, START, NIT = (int(v) for v in sys.argv[1:5])
+os.environ.setdefault("PHGPU_VERBOSE", "1")
 opts = {"solvername": "mi355x_pdhg", "PHIterLimit": 100000, "defaultPHrho": 1.0,
         "convthresh": -1, "verbose": False, "display_progress": False,
         "iter0_solver_options": {}, "iterk_solver_options": {}, "device_loop_graphs": False}
-ph = PH(opts, [f"scen{i}" for i in range(S)], farmer.scenario_creator,
-        scenario_creator_kwargs={"crops_multiplier": C})
+if C == 0:
+    ph = PH(opts, sslp.scenario_names(S), sslp.scenario_creator,
+            scenario_creator_kwargs={"instance": "sslp_15_45_synthetic"})
+else:
+    ph = PH(opts, [f"scen{i}" for i in range(S)], farmer.scenario_creator,
+            scenario_creator_kwargs={"crops_multiplier": C})
 ph.PH_Prep(); ph.subproblem_creation(); ph.Iter0()
 ph.run_device_loop(0, START, -1.0)
 b = ph.batch
@@ -34,6 +39,11 @@ t = b.read_timing_full()
 lib.ph_debug_prof(b.handle, 0, out.ctypes.data_as(ctypes.c_void_p))
 us = lambda v: v / 100.0  # 100 MHz ticks -> us (summed over blocks)
 npol = max(out[9], 1)
+st = b.loop_status()  # (counters since run_device_loop's reset: these NIT passes)
+steps = int(st[4])
+grid = 0
+print(f"PDHG steps over the {NIT} passes: {steps} (last pass max {int(b.iters.max().item())}); "
+      f"mid_kernel ms per 1000 steps: {t[5] / max(steps, 1) * 1000:.3f}")
 print(f"iters {START}..{START+NIT}: mid_kernel {t[4]} launches {t[5]/max(t[4],1):.3f} ms avg, "
       f"mid_polish {t[6]} launches {t[7]/max(t[6],1):.3f} ms avg")
 print(f"polishes {out[9]} ({out[9]/NIT:.0f}/iter), rounds {out[10]}, refinement solves {out[11]}, "
