@@ -3575,15 +3575,20 @@ bool pick_mid(int n, int m, int *blk, int *pc, int *pr) {
   } while (0)
 
 // Tails of the lines longer than LINE_D for a BLOCK-thread geometry:
-// grouped by the owner's wave (line l is owned by thread l % BLOCK, slot
-// l / BLOCK), see Tails.
-void build_tails(int lines, const int32_t *ptr, int BLOCK, std::vector<int32_t> &wp,
+// grouped by the owner's wave (line l is owned by slot l / BLOCK of thread
+// l % BLOCK, or with `inter` of thread (r % NW) WAVE + r / NW, r = l % BLOCK:
+// MidArgs::rint), see Tails.
+void build_tails(int lines, const int32_t *ptr, int BLOCK, bool inter, std::vector<int32_t> &wp,
                  std::vector<int32_t> &tb, std::vector<int32_t> &ln, std::vector<int32_t> &bb,
                  std::vector<int32_t> &tpos) {
   const int NW = BLOCK / WAVE;
+  auto owner = [&](int l) {
+    const int r = l % BLOCK;
+    return inter ? (r % NW) * WAVE + r / NW : r;
+  };
   std::vector<std::vector<int>> per_wave(NW);
   for (int l = 0; l < lines; ++l)
-    if (ptr[l + 1] - ptr[l] > LINE_D) per_wave[(l % BLOCK) / WAVE].push_back(l);
+    if (ptr[l + 1] - ptr[l] > LINE_D) per_wave[owner(l) / WAVE].push_back(l);
   wp.assign(NW + 1, 0);
   tb.assign(1, 0);
   ln.clear();
@@ -3591,7 +3596,7 @@ void build_tails(int lines, const int32_t *ptr, int BLOCK, std::vector<int32_t> 
   tpos.clear();
   for (int w = 0; w < NW; ++w) {
     for (int l : per_wave[w]) {
-      ln.push_back((l % BLOCK) % WAVE);
+      ln.push_back(owner(l) % WAVE);
       bb.push_back(l / BLOCK);
       for (int p = ptr[l] + LINE_D; p < ptr[l + 1]; ++p) tpos.push_back(p);
       tb.push_back((int32_t)tpos.size());
@@ -3693,8 +3698,12 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   long common = 0, ws = 0;
   bool ws_lds = false;
   if (!big) {
-    build_tails(b->m, row_ptr, b->mblock, rwp, rtb, rln, rbb, rtp);
-    build_tails(b->n, col_ptr.data(), b->mblock, cwp, ctb, cln, cbb, ctp);
+    // (rows fewer than the block: interleaved over its waves, MidArgs::rint;
+    // PHGPU_MID_RINT=0: measurement hook, off)
+    const char *ri = std::getenv("PHGPU_MID_RINT");
+    b->md.rint = b->m < b->mblock && !(ri && std::atoi(ri) == 0) ? 1 : 0;
+    build_tails(b->m, row_ptr, b->mblock, b->md.rint != 0, rwp, rtb, rln, rbb, rtp);
+    build_tails(b->n, col_ptr.data(), b->mblock, false, cwp, ctb, cln, cbb, ctp);
     // LDS plan (doubles): see the carve at the top of solve_mid
     const long nw = b->mblock / WAVE;
     auto meta = [&](long nlong) { return nw + 1 + nlong + 1 + 2 * nlong; };

@@ -55,3 +55,6 @@ print(f"rounds with a pinned row {out[5]}; exits: accepted {out[12]}, set repeat
 print(f"set repeats failing only the gap {out[20]}, rounds with a slack pinned row {out[21]}")
 print(f"factorisations with a pivot held to its bound {out[16]}; non-finite: rhs {out[17]}, "
       f"refinement solve {out[18]}, check only {out[19]}")
+nsc = max(out[30], 1)
+print(f"PDHG phases: scenarios {out[30]}, steps {out[29]}; block-us per scenario: setup {us(out[22])/nsc:.1f} "
+      f"end {us(out[31])/nsc:.1f}; per step: {us(out[23])/max(out[29],1):.2f} (+ checks {us(out[24])/max(out[29],1):.2f})")
