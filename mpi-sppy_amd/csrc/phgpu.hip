@@ -3702,6 +3702,10 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     // PHGPU_MID_RINT=0: measurement hook, off)
     const char *ri = std::getenv("PHGPU_MID_RINT");
     b->md.rint = b->m < b->mblock && !(ri && std::atoi(ri) == 0) ? 1 : 0;
+    // (PHGPU_MID_PK16=0: measurement hook, the polish's products read the
+    // pattern from L2 as before)
+    const char *pk = std::getenv("PHGPU_MID_PK16");
+    b->md.pk16 = b->n < 65535 && b->m < 65535 && b->nnz < 65535 && !(pk && std::atoi(pk) == 0) ? 1 : 0;
     build_tails(b->m, row_ptr, b->mblock, b->md.rint != 0, rwp, rtb, rln, rbb, rtp);
     build_tails(b->n, col_ptr.data(), b->mblock, false, cwp, ctb, cln, cbb, ctp);
     // LDS plan (doubles): see the carve at the top of solve_mid
