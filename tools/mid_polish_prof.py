@@ -51,6 +51,7 @@ print(f"polishes {out[9]} ({out[9]/NIT:.0f}/iter), rounds {out[10]}, refinement 
 print(f"per polish (block-us): setup {us(out[15] + out[27])/npol:.1f} (scatter {us(out[27])/npol:.1f}) "
       f"factor {us(out[13])/npol:.1f} solves {us(out[14])/npol:.1f} check {us(out[25])/npol:.1f} "
       f"PDAS {us(out[26])/npol:.1f}")
+print(f"factors reused from the cache {out[28]} (of {out[10]} rounds)")
 print(f"rounds with a pinned row {out[5]}; exits: accepted {out[12]}, set repeats {out[1]}, non-finite {out[2]}, round limit {out[3]}; "
       f"failed checks: refinement short {out[4]}, ep {out[6]}, ed {out[7]}, eg {out[8]}")
 print(f"set repeats failing only the gap {out[20]}, rounds with a slack pinned row {out[21]}")
