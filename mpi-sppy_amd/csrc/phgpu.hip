@@ -1801,6 +1801,27 @@ __device__ __forceinline__ int as_eval(const SolveArgs &a, int s, int lane, cons
   return AS_HIT;
 }
 
+// An accepted solve's outputs held back for the persistent loop (its
+// lagged convergence test may discard the pass): a scenario's pending slot
+// [x n][y m][pobj, dbound, ep, ed, eg, how, valid], scaled back already.
+__host__ __device__ constexpr int pend_width(int n, int m) { return (n + m + 8) & ~1; }
+__device__ __forceinline__ void pend_put(double *pd, int n, int m, int hl, bool cn, bool cm, double xv,
+                                         double yv, double pobj, double dobj, double ep, double ed,
+                                         double eg, double how) {
+  if (cn) pd[hl] = xv;
+  if (cm) pd[n + hl] = yv;
+  if (hl == 0) {
+    double *t = pd + n + m;
+    t[0] = pobj;
+    t[1] = dobj;
+    t[2] = ep;
+    t[3] = ed;
+    t[4] = eg;
+    t[5] = how;
+    t[6] = 1.0;
+  }
+}
+
 // Sum over this lane's group of LPS lanes (16: one DPP row, 32: a half
 // wave), uniform within the group.  The DPP steps stay inside 16-lane rows
 // (after them every lane holds its row's sum); a 32-lane group adds its two
@@ -1833,7 +1854,8 @@ __device__ __forceinline__ void as_evalg(const SolveArgs &a, int s0, const int (
                                          const double *ENT, const double *SBV, const double *VLV,
                                          const int32_t *OKV, const Pattern &P, double *xsw, double hk_l,
                                          double qk_l, double cst_l, int kslot, double &XN_out,
-                                         int (&r)[64 / LPS], unsigned long long (&sig)[64 / LPS][4]) {
+                                         int (&r)[64 / LPS], unsigned long long (&sig)[64 / LPS][4],
+                                         double *PEND) {
   constexpr int NG = 64 / LPS;
   constexpr unsigned long long GM = LPS == 32 ? 0xffffffffull : 0xffffull;
   const int S = a.S, n = a.n, m = a.m, K = a.K, VL = cache_vlen(n, m), CW = a.CW, SBW = 4 * n + 3 * m;
@@ -1921,7 +1943,10 @@ __device__ __forceinline__ void as_evalg(const SolveArgs &a, int s0, const int (
     for (int i = 0; i < 4; ++i) sig[q][i] = (sg[i] >> (q * LPS)) & GM;
     r[q] = nog[q] ? AS_NOENTRY : (((am >> (q * LPS)) & 1ull) ? AS_HIT : AS_MOVED);
   }
-  if (acc) {
+  if (acc && PEND) {  // (the persistent loop: held back, slot j of the wave's pending area)
+    pend_put(PEND + (size_t)j * pend_width(n, m), n, m, hl, cn, cm, XN * DC, YN * DR, pobj, dobj, ep, ed, eg,
+             3.0);
+  } else if (acc) {
     if (cn) a.x[(size_t)hl * S + s] = XN * DC;
     if (cm) a.y[(size_t)hl * S + s] = YN * DR;
     if (hl == 0) {
@@ -2196,7 +2221,7 @@ __device__ __forceinline__ bool polish_one(const SolveArgs &a, int s, int lane, 
                                            const PatLds &pt, const double *vl, const double *sb,
                                            double hk_l, double qk_l, double cst_l, int kslot,
                                            const unsigned long long (&sig0)[4], double *ent2,
-                                           double &XN_out) {
+                                           double &XN_out, double *pend = nullptr) {
   const int S = a.S, n = a.n, m = a.m, K = a.K;
   double *kst = w.kst, *sol = w.sol, *xs = w.xs, *ys = w.ys;
   int32_t *cpos = w.cpos, *rpos = w.rpos;
@@ -2434,6 +2459,11 @@ __device__ __forceinline__ bool polish_one(const SolveArgs &a, int s, int lane, 
       }
       tick(14);  // cache store
       if (a.prof && lane == 0) atomicAdd(&a.prof[15], 1ull);
+      if (pend) {  // (the persistent loop: held back)
+        pend_put(pend, n, m, lane, lane < n, lane < m, xn * DC, yn * DR, pobj, dobj, ep, ed, eg, 1.0);
+        XN_out = xn;
+        return true;
+      }
       if (lane < n) a.x[(size_t)lane * S + s] = xn * DC;
       if (lane < m) a.y[(size_t)lane * S + s] = yn * DR;
       if (lane == 0) {
@@ -2949,19 +2979,19 @@ struct LoopLds {
   int pat, blk, wave, total;   // sizes in doubles
   // per-wave offsets (doubles) inside a wave's slice
   int o_kst, o_sol, o_xs, o_ys, o_acc, o_ent, o_sb, o_vl, o_rho, o_w, o_pc, o_wc, o_xb, o_xn,
-      o_wcv, o_int;
+      o_wcv, o_pend, o_int;
 };
 __host__ __device__ inline LoopLds loop_lds(int n, int m, int nnz, int K, int G, int CW, int spw) {
   LoopLds L{};
   const int pat_ints = (m + 1) + (n + 1) + 3 * nnz;
   L.pat = (pat_ints + 1) / 2;
-  L.blk = 256 + (2 * G + 2) + 8;  // combine scratch, sums + counts, flags
+  L.blk = 256 + 2 * (2 * G + 3) + 8;  // combine scratch, sums, the next sums + counts + conv, flags
   int o = 0;
   L.o_kst = o; o += RG_KST;
   L.o_sol = o; o += (1 + RG_K) * WAVE;
   L.o_xs = o; o += WAVE;
   L.o_ys = o; o += WAVE;
-  L.o_acc = o; o += 2 * G + 2;
+  L.o_acc = o; o += 2 * G + 4;
   L.o_ent = o; o += spw * CW;
   L.o_sb = o; o += spw * (4 * n + 3 * m);
   L.o_vl = o; o += spw * nnz;
@@ -2972,6 +3002,7 @@ __host__ __device__ inline LoopLds loop_lds(int n, int m, int nnz, int K, int G,
   L.o_xb = o; o += spw * K;
   L.o_xn = o; o += spw * K;
   L.o_wcv = o; o += spw;
+  L.o_pend = o; o += spw * pend_width(n, m);
   L.o_int = o; o += (2 * WAVE + spw * (K + 1) + 1) / 2;  // cpos, rpos, gid [spw][K], ok [spw]
   L.wave = o;
   L.total = L.pat + L.blk + LOOP_WPB * L.wave;
@@ -3059,7 +3090,7 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
   const SolveArgs &a = L.a;
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   const int S = a.S, n = a.n, m = a.m, nnz = a.nnz, K = a.K, G = L.G, CW = a.CW;
-  const int SBW = 4 * n + 3 * m, PQ = 2 * G + 2;
+  const int SBW = 4 * n + 3 * m, PQ = 2 * G + 3, PW = pend_width(n, m);
   LoopCtl *ctl = L.ctl;
   const int stop0 = *(volatile int32_t *)&ctl->stop;
   int it = *(volatile int32_t *)&ctl->iter;
@@ -3070,12 +3101,14 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
   int32_t *rp = (int32_t *)lds, *ci = rp + (m + 1), *cp = ci + nnz, *cr = cp + (n + 1), *ck = cr + nnz;
   double *blk = lds + lay.pat;
   double *scr = blk;                 // [256] combine scratch
-  double *sums_l = blk + 256;        // [2G] sums, [2G] misses, [2G+1] tails
-  int *flag = (int *)(sums_l + PQ);  // barrier result
+  double *sums_l = blk + 256;        // [2G] this pass's sums
+  double *nxt = sums_l + PQ;         // combined: [2G] the next sums, [2G] misses, [2G+1] tails, [2G+2] conv
+  int *flag = (int *)(nxt + PQ);     // barrier result
   double *wv = lds + lay.pat + lay.blk + (size_t)w * lay.wave;
   double *ENT = wv + lay.o_ent, *SBV = wv + lay.o_sb, *VLV = wv + lay.o_vl;
   double *RHO = wv + lay.o_rho, *WW = wv + lay.o_w, *PCV = wv + lay.o_pc, *WCV = wv + lay.o_wc;
   double *XBV = wv + lay.o_xb, *XNV = wv + lay.o_xn, *WCONV = wv + lay.o_wcv, *ACC = wv + lay.o_acc;
+  double *PEND = wv + lay.o_pend;  // [spw][PW] the pass's accepted solutions, held back
   int32_t *ints = (int32_t *)(wv + lay.o_int);
   int32_t *cpos = ints, *rpos = ints + WAVE, *GID = ints + 2 * WAVE, *OKV = GID + L.spw * K;
   const PolScratch ws{wv + lay.o_kst, wv + lay.o_sol, wv + lay.o_xs, wv + lay.o_ys, cpos, rpos};
@@ -3116,6 +3149,7 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
       if (lane == 0) {
         WCONV[j] = L.wconv[s];
         OKV[j] = a.cache_ok[s];
+        PEND[(size_t)j * PW + n + m + 6] = 0.0;
       }
     }
   }
@@ -3160,35 +3194,15 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
       if (lane == 0) L.absdiff[s] = ad;
       convw += ad * WCONV[j];
     }
-    if (lane == 0) scr[w] = convw;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double t = 0.0;
-      for (int q = 0; q < LOOP_WPB; ++q) t += scr[q];
-      pub(L.part_c + blockIdx.x, t);
-      tick(0);
-      if (blockIdx.x == 0) {  // the pass's work-list counters (before any push: barrier)
-        __hip_atomic_store(L.ctr + 0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(L.ctr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(L.ctr + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(L.ctr + 6, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (!grid_sync(L.bar, gen, flag, a.err)) {
-      aborted = true;
-      break;
-    }
-    tick(1);
-    grid_combine(L.part_c, 1, 1, scr, sums_l + 2 * G);
-    tick(2);
-    const double conv = sums_l[2 * G];
-    if (threadIdx.x == 0 && blockIdx.x == 0) L.hist[it - 1] = conv;
-    if (conv < thresh) {
-      stop = 1;
-      break;
-    }
+    tick(0);
+    // Lagged convergence test: this pass's conv partial travels with the
+    // solve's partials (one grid barrier per pass); the solve below is
+    // speculative, its outputs held back (PEND) until the combined conv
+    // shows the reference would have run it (phbase.py:1517-1530: the
+    // convergence test precedes the solve), else discarded.
     // ================= S: the solve of the owned scenarios
     for (int q = lane; q < 2 * G; q += WAVE) ACC[q] = 0.0;
+    if (lane == 0) ACC[2 * G + 2] = convw;
     int nmiss = 0, ntail = 0, npol = 0;
     wsync();
     // 64 / LPS owned scenarios per wave at a time (as_evalg, one group of
@@ -3206,7 +3220,7 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
       double XN2 = 0.0;
       int rr[NG];
       unsigned long long sg[NG][4];
-      as_evalg<LPS>(a, s0, jg, lane, ENT, SBV, VLV, OKV, Pl, ws.xs, hk2, qk2, cst2, kslotg, XN2, rr, sg);
+      as_evalg<LPS>(a, s0, jg, lane, ENT, SBV, VLV, OKV, Pl, ws.xs, hk2, qk2, cst2, kslotg, XN2, rr, sg, PEND);
       for (int u = 0; u < NG; ++u) {
         const int jc = jg[u];
         if (jc < 0) break;
@@ -3234,7 +3248,7 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
           const unsigned long long tp0 = L.prof ? wall_clock64() : 0ull;
           double XN = 0.0;
           solved = polish_one(a, s, lane, ws, pt, vl_j, sb_j, hk_l, qk_l, cst_l, kslot, sig,
-                              ENT + (size_t)jc * CW, XN);
+                              ENT + (size_t)jc * CW, XN, PEND + (size_t)jc * PW);
           if (L.prof) {
             tpol += wall_clock64() - tp0;
             ++npolw;
@@ -3280,18 +3294,56 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
       break;
     }
     tick(4);
-    grid_combine(L.part_x, PQ, PQ, scr, sums_l);
+    grid_combine(L.part_x, PQ, PQ, scr, nxt);
     tick(2);
+    const double conv = nxt[2 * G + 2];
+    if (threadIdx.x == 0 && blockIdx.x == 0) L.hist[it - 1] = conv;
+    if (conv < thresh) {  // converged before this pass's solve: its outputs are dropped
+      stop = 1;
+      break;
+    }
+    // commit the held-back solutions of the wave's scenarios, lanes over
+    // (element, scenario) so consecutive lanes store consecutive scenarios
+    // of the [n][S] / [m][S] arrays (one store per 64 values, not per lane)
+    for (int q = lane; q < ns * n; q += WAVE) {
+      const int e = q / ns, j = q - e * ns;
+      const double *pd = PEND + (size_t)j * PW;
+      if (pd[n + m + 6] != 0.0) a.x[(size_t)e * S + s0 + j] = pd[e];
+    }
+    for (int q = lane; q < ns * m; q += WAVE) {
+      const int e = q / ns, j = q - e * ns;
+      const double *pd = PEND + (size_t)j * PW;
+      if (pd[n + m + 6] != 0.0) a.y[(size_t)e * S + s0 + j] = pd[n + e];
+    }
+    for (int j = lane; j < ns; j += WAVE) {
+      double *t = PEND + (size_t)j * PW + n + m;
+      if (t[6] == 0.0) continue;
+      const int s = s0 + j;
+      a.status[s] = PH_STATUS_OPTIMAL;
+      a.iters[s] = 0;
+      a.pobj[s] = t[0];
+      a.dbound[s] = t[1];
+      double *dg = a.diag + PH_DIAG_W * (size_t)s;
+      dg[0] = t[2];
+      dg[1] = t[3];
+      dg[2] = t[4];
+      dg[3] = -1.0;
+      dg[4] = t[5];
+    }
+    wsync();  // (the flags read above, then cleared)
+    for (int j = lane; j < ns; j += WAVE) PEND[(size_t)j * PW + n + m + 6] = 0.0;
     n_pol += (unsigned long long)npol;
     n_hit += (unsigned long long)(ns - nmiss);
-    if (sums_l[2 * G + 1] > 0.0) {  // a tail: the host-queued kernels finish this pass
+    if (nxt[2 * G + 1] > 0.0) {  // a tail: the host-queued kernels finish this pass
       tail = 1;
       if (threadIdx.x == 0 && blockIdx.x == 0)
-        __hip_atomic_store(L.ctr + 0, (int)sums_l[2 * G], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(L.ctr + 0, (int)nxt[2 * G], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       n_pol -= (unsigned long long)npol;  // (summary_kernel counts this pass)
       n_hit -= (unsigned long long)(ns - nmiss);
       break;
     }
+    for (int q = threadIdx.x; q < 2 * G; q += blockDim.x) sums_l[q] = nxt[q];
+    __syncthreads();
     ++passes;
     if (it >= limit) {
       stop = 2;
@@ -4960,8 +5012,11 @@ static int loop_persist_setup(ph_batch *b, bool *ok) {
   return PH_OK;
 }
 
-__global__ void __launch_bounds__(WAVE) loop_prep_kernel(LoopCtl *c, int32_t *bar, int iters, int first) {
+__global__ void __launch_bounds__(WAVE) loop_prep_kernel(LoopCtl *c, int32_t *bar, int32_t *ctr, int iters,
+                                                         int first) {
   for (int q = threadIdx.x; q < LBAR_WORDS; q += WAVE) bar[q] = 0;
+  // the work-list counters (a loop pass pushes only when it ends the launch)
+  if (threadIdx.x == 0) ctr[0] = ctr[1] = ctr[2] = ctr[6] = 0;
   if (first && threadIdx.x == 0) c->iter_end = c->iter + iters;
 }
 
@@ -5040,7 +5095,7 @@ int ph_loop_run(ph_batch_t b, int32_t iters) {
   constexpr int ROUNDS = 4;
   const int post_g = b->loop_xa.G * std::max(1, b->loop_xa.C);
   for (int r = 0; r < ROUNDS; ++r) {
-    hipLaunchKernelGGL(loop_prep_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_ctl, b->d_lbar, (int)iters,
+    hipLaunchKernelGGL(loop_prep_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_ctl, b->d_lbar, b->d_ctr, (int)iters,
                        r == 0 ? 1 : 0);
     if (int rc = phase_event(b, 2)) return rc;
     if (b->n <= 16 && b->m <= 16)
