@@ -340,11 +340,14 @@ int ph_loop_pass(ph_batch_t b);
  * and of conv).  With one rank and the one-wave cached warm solve, once
  * ph_loop_status has seen a quiet stretch (no PDHG tail, at most 2e-3 cache
  * misses per scenario-pass since its previous read; PHGPU_PERSIST=1 / 0
- * forces the choice): a persistent launch runs whole passes with two grid barriers each (Compute_Xbar
- * broadcast + Update_W + conv, then the cached map / register polish of every
- * scenario and the next sums) while the owned scenarios' data stay in LDS;
- * a pass with a polish failure is finished by the tail and post-solve
- * kernels queued behind it (up to four such rounds per call).  Otherwise
+ * forces the choice): a persistent launch runs whole passes with one grid
+ * barrier each (Compute_Xbar broadcast + Update_W + the conv partial, the
+ * cached map / register polish of every scenario held back in LDS, the next
+ * sums; after the barrier the combined conv either drops the pass's solve --
+ * the reference tests before it solves -- or commits it) while the owned
+ * scenarios' data stay in LDS; a pass with a polish failure is finished by
+ * the tail and post-solve kernels queued behind it (up to four such rounds
+ * per call).  Otherwise
  * `iters` ph_loop_pass calls.  The caller reads ph_loop_status for how far
  * it got.  Replaces: iterk_loop's loop body (phbase.py:1498-1553) repeated.
  */
