@@ -3173,7 +3173,39 @@ __global__ void __launch_bounds__(LOOP_WPB * WAVE) loop_kernel(LoopArgs L) {
   while (ok) {
     // ================= U: Compute_Xbar broadcast, Update_W, conv partial
     double convw = 0.0;
-    for (int j = 0; j < ns; ++j) {
+    if (ns * K <= WAVE) {
+      // every (scenario, slot) pair on its own lane: one round of loads and
+      // stores; the per-scenario |d| sums (in slot order) and the conv terms
+      // (in scenario order, lane 0) as the loop below adds them
+      double *ADV = ws.ys, *CWV = ws.xs;
+      if (lane < ns * K) {
+        const int j = lane / K, k = lane - j * K, s = s0 + j;
+        const size_t o = (size_t)k * S + s;
+        const int g = GID[lane];
+        const double xb = sums_l[g], xsq = sums_l[G + g];
+        L.xbar[o] = xb;
+        L.xsqbar[o] = xsq;
+        XBV[lane] = xb;
+        const double d = XNV[lane] - xb;
+        double wn = WW[lane] + RHO[lane] * d;
+        if (L.wc) wn *= WCV[lane];
+        WW[lane] = wn;
+        L.W[o] = wn;
+        ADV[lane] = fabs(d);
+      }
+      wsync();
+      if (lane < ns) {
+        double ad = 0.0;
+        for (int k = 0; k < K; ++k) ad += ADV[lane * K + k];
+        L.absdiff[s0 + lane] = ad;
+        CWV[lane] = ad * WCONV[lane];
+      }
+      wsync();
+      if (lane == 0)
+        for (int j = 0; j < ns; ++j) convw += CWV[j];
+      convw = __shfl(convw, 0, WAVE);
+    }
+    for (int j = 0; j < (ns * K <= WAVE ? 0 : ns); ++j) {
       const int s = s0 + j;
       double ad = 0.0;
       if (lane < K) {
