@@ -4215,6 +4215,39 @@ static int phase_event(ph_batch *b, int kind) {
   return PH_OK;
 }
 
+// Kernels whose blocks wait for each other (the persistent loop's grid
+// barrier, the big path's team barriers) go through a cooperative launch:
+// the runtime either places every block of the grid at once or refuses the
+// launch, instead of a plain launch that can leave blocks waiting for CUs
+// held by another stream's (a spoke's) spinning kernel until the barrier's
+// tick budget aborts.  A stream being captured into a graph takes the plain
+// launch (graphs are opt-in and single-cylinder);
+// PHGPU_COOP=0: plain launches (measurement hook).  *placed = false: the
+// cooperative launch was refused as too large (the caller falls back).
+static bool coop_enabled() {
+  const char *e = std::getenv("PHGPU_COOP");
+  return !(e && *e && std::atoi(e) == 0);
+}
+
+static int launch_coop(const void *f, dim3 grid, dim3 block, void **args, size_t lds, hipStream_t s,
+                       bool *placed) {
+  *placed = true;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_OK(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone || !coop_enabled()) {
+    HIP_OK(hipLaunchKernel(f, grid, block, args, lds, s));
+    return PH_OK;
+  }
+  const hipError_t e = hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)lds, s);
+  if (e == hipErrorCooperativeLaunchTooLarge) {
+    (void)hipGetLastError();
+    *placed = false;
+    return PH_OK;
+  }
+  if (e != hipSuccess) return fail(PH_EHIP, std::string("hipLaunchCooperativeKernel: ") + hipGetErrorString(e));
+  return PH_OK;
+}
+
 // PHGPU_MID_FULLGRID=1: measurement hook, the phase kernels launched over S
 // blocks (one scenario each) instead of the resident grid
 static bool mid_full_grid() {
@@ -4268,9 +4301,10 @@ static int big_init(ph_batch *b) {
   b->bg.team_bar = b->bg.team_abort = nullptr;
   b->bg.team_part = nullptr;
   const char *te = std::getenv("PHGPU_BIG_TEAMS");
-  int per_cu_t = 0;
+  int per_cu_t = 0, coop = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, big_team_kernel, BIG_BLOCK, BIG_SMALL_LDS));
-  if (!(te && std::atoi(te) == 0) && !mid_grid_cap() && per_cu_t >= 1) {
+  HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
+  if (!(te && std::atoi(te) == 0) && !mid_grid_cap() && per_cu_t >= 1 && (coop || !coop_enabled())) {
     // every block of the launch resident: a team's barrier needs all of it
     const int tg = std::min(std::max(1, per_cu), per_cu_t) * std::max(1, cus);
     if ((rc = dalloc(&b->d_teambar, (size_t)tg + 1)) ||
@@ -4415,10 +4449,19 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
       else
         hipLaunchKernelGGL(big_kernel<false>, dim3(b->big_tgrid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
                            a, b->bg, ph);
-      if (b->bg.team_bar)  // (exits at once unless the phase's list is short)
-        hipLaunchKernelGGL(big_team_kernel, dim3(b->big_tgrid), dim3(BIG_BLOCK), BIG_SMALL_LDS, b->stream, a,
-                           b->bg, ph);
       HIP_OK(hipGetLastError());
+      if (b->bg.team_bar) {  // (exits at once unless the phase's list is short)
+        SolveArgs ta = a;
+        BigArgs tb = b->bg;
+        MidPhase tp = ph;
+        void *args[3] = {&ta, &tb, &tp};
+        bool placed = true;
+        if (int rc = launch_coop((const void *)big_team_kernel, dim3(b->big_tgrid), dim3(BIG_BLOCK), args,
+                                 BIG_SMALL_LDS, b->stream, &placed))
+          return rc;
+        if (!placed)  // big_kernel already ran with teams on: the list would be left unsolved
+          return fail(PH_EHIP, "big_team_kernel: cooperative launch refused (grid not co-resident)");
+      }
       return phase_event(b, -1);
     }
     DISPATCH_MID({
@@ -5015,9 +5058,11 @@ static int loop_persist_setup(ph_batch *b, bool *ok) {
       b->loop_xa.out != p.sums)
     return PH_OK;
   if (b->loop_grid == 0 || b->loop_G != p.G) {
-    int cus = 0, dev = 0, per_cu = 0;
+    int cus = 0, dev = 0, per_cu = 0, coop = 0;
     HIP_OK(hipGetDevice(&dev));
     HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
+    if (!coop && coop_enabled()) return PH_OK;  // no cooperative launch: the per-pass kernels
     const int NB = std::max(1, std::min(cus, (b->S + LOOP_WPB - 1) / LOOP_WPB));
     const int NW = NB * LOOP_WPB;
     const int spw = (b->S + NW - 1) / NW;
@@ -5130,11 +5175,15 @@ int ph_loop_run(ph_batch_t b, int32_t iters) {
     hipLaunchKernelGGL(loop_prep_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_ctl, b->d_lbar, b->d_ctr, (int)iters,
                        r == 0 ? 1 : 0);
     if (int rc = phase_event(b, 2)) return rc;
-    if (b->n <= 16 && b->m <= 16)
-      hipLaunchKernelGGL(loop_kernel<16>, dim3(b->loop_grid), dim3(LOOP_WPB * WAVE), b->loop_lds_bytes, b->stream, L);
-    else
-      hipLaunchKernelGGL(loop_kernel<32>, dim3(b->loop_grid), dim3(LOOP_WPB * WAVE), b->loop_lds_bytes, b->stream, L);
-    HIP_OK(hipGetLastError());
+    {
+      const void *kf = (b->n <= 16 && b->m <= 16) ? (const void *)loop_kernel<16> : (const void *)loop_kernel<32>;
+      void *args[1] = {&L};
+      bool placed = true;
+      if (int rc = launch_coop(kf, dim3(b->loop_grid), dim3(LOOP_WPB * WAVE), args, b->loop_lds_bytes, b->stream,
+                               &placed))
+        return rc;
+      if (!placed) return fail(PH_EHIP, "loop_kernel: cooperative launch refused (grid not co-resident)");
+    }
     if (int rc = phase_event(b, -1)) return rc;
     if (int rc = launch_tail(b, a, lds)) return rc;
     hipLaunchKernelGGL(summary_kernel, dim3(1 + post_g), dim3(1024), 0, b->stream, b->S, p.status, p.iters,

@@ -14,9 +14,11 @@ MI355X form: the bundles of a rank are a second scenario-batched layout
 whose "scenario" is a bundle.  Every bundle has the same shape -- T blocks
 (T = the largest bundle; a shorter bundle's last block is inert: its columns
 fixed at 0, its rows free) of the scenario pattern plus (T - 1) x K
-nonanticipativity rows x_t[k] - x_(t-1)[k] = 0, active when blocks t-1 and t
-belong to the same tree node at slot k (a node's scenarios are contiguous,
-so the chain of equalities is the reference's star x_t = x_ref).  The batched
+nonanticipativity rows x_t[k] - x_ref[k] = 0: the reference's star on the
+bundle's first scenario (x_ref = block 0) where slot k is at one node for
+every scenario (two-stage), else a chain x_ref = x_(t-1) (a node's scenarios
+are contiguous), active when both blocks belong to slot k's node and block
+t's nonant is not fixed (nonant_for_fixed_vars=False).  The batched
 solver runs on that layout unchanged; its PH terms are gathered from the
 scenario arrays with the EF weights p_s / P_b, and its solution is scattered
 back to the scenarios' x (``ph_gather`` in include/phgpu.h).
@@ -91,9 +93,14 @@ class BundleLayout:
         base = T * nnz
         L = (T - 1) * K
         row_ptr.append(base + 2 * np.arange(L))
+        # slot k's link rows: a star on block 0 (the reference's ref_vars,
+        # sputils.py:350-363: the bundle's first scenario) when every scenario
+        # has slot k at the same node (two-stage); else a chain t-1 -> t (a
+        # node's scenarios are contiguous)
+        star = np.all(gid == gid[:, :1], axis=1) if S > 0 else np.ones(K, dtype=bool)
         link_cols = np.empty((T - 1, K, 2), dtype=np.int64)
         for t in range(1, T):
-            link_cols[t - 1, :, 0] = (t - 1) * n + nc
+            link_cols[t - 1, :, 0] = np.where(star, 0, t - 1) * n + nc
             link_cols[t - 1, :, 1] = t * n + nc
         col_idx.append(link_cols.reshape(-1))
         row_ptr = np.concatenate(row_ptr + [[base + 2 * L]])
@@ -112,12 +119,18 @@ class BundleLayout:
         ub = take(data.u, 0.0)
         rl = take(data.rl, -np.inf)
         ru = take(data.ru, np.inf)
-        # link rows: active when blocks t-1, t are real and share slot k's node
+        # link rows: active when both blocks are real and share slot k's node,
+        # and the later block's nonant is not fixed in its scenario (the bundle
+        # EF is formed with nonant_for_fixed_vars=False, phbase.py:860-861,
+        # sputils.py:358-360: no row for a fixed Var)
         gext = np.concatenate([gid, np.full((K, 1), -1)], axis=1)
+        fixed = np.concatenate([data.l[nc] == data.u[nc], np.ones((K, 1), dtype=bool)], axis=1)  # [K][S+1]
         lrl = np.full((T - 1, K, Sb), -np.inf)
         for t in range(1, T):
-            same = real[t][None, :] & real[t - 1][None, :] & \
-                (gext[:, member[t]] == gext[:, member[t - 1]])
+            mr = np.where(star[:, None], member[0][None, :], member[t - 1][None, :])   # [K][Sb]
+            rr = np.where(star[:, None], real[0][None, :], real[t - 1][None, :])
+            same = real[t][None, :] & rr & (np.take_along_axis(gext, mr, axis=1) == gext[:, member[t]]) & \
+                ~fixed[:, member[t]]
             lrl[t - 1] = np.where(same, 0.0, -np.inf)
         lru = np.where(np.isfinite(lrl), 0.0, np.inf)
         rl = np.concatenate([rl, lrl.reshape(L, Sb)], axis=0)

@@ -288,13 +288,16 @@ class PHBase(SPBase):
         self._b_of = torch.as_tensor(bl.bundle_of, dtype=torch.int64, device=dev)
         self._b_scal = torch.zeros(1, **f64)
 
-    def _launch_solve(self, kw):
+    def _launch_solve(self, kw, use_scenarios=False):
         """Queue the batched solve of every local subproblem.  With bundles:
         the bundle batch's PH terms gathered from the scenario arrays with
         the EF weights p_s / P_b, the bundle solve, and its solution
         scattered to the scenarios' x (the scenario sub-blocks hold the EF
-        solution, phbase.py:833-838); one ph_gather call per array."""
-        if not self.bundling:
+        solution, phbase.py:833-838); one ph_gather call per array.
+        ``use_scenarios``: solve_loop's use_scenarios_not_subproblems
+        (phbase.py:1038-1041): the scenario batch even when bundling."""
+        self._solved_scenarios = use_scenarios or not self.bundling
+        if self._solved_scenarios:
             self.batch.solve(self.W, self.rho, self.xbar, self.w_on, self.prox_on, **kw)
             return
         bb = self.bbatch
@@ -309,17 +312,19 @@ class PHBase(SPBase):
         """(not optimal, PDHG iterations sum, max, polished, cached) of the
         last solve (waits for it); with bundles the bundle solve's, and the
         bundle statuses copied to their scenarios (phbase.py:992-995)."""
-        if not self.bundling:
+        if getattr(self, "_solved_scenarios", True):
             return self.batch.summary()
         out = self.bbatch.summary()
         ts = getattr(self.batch, "torch_stream", None)
         with torch.cuda.stream(ts) if ts is not None else _nullctx():
             self.batch.status.copy_(self.bbatch.status.index_select(0, self._b_of))
+        if ts is not None:  # host reads of batch.status (on the current stream) after the copy
+            torch.cuda.current_stream(self.device).wait_stream(ts)
         return out
 
     @property
     def n_subproblems(self):
-        return self.bundle_layout.Sb if self.bundling else self.S_loc
+        return self.S_loc if getattr(self, "_solved_scenarios", True) else self.bundle_layout.Sb
 
     # ----------------------------------------------------------- solves --
     def solve_loop_launch(self, solver_options=None, dis_W=False, dis_prox=False):
@@ -369,7 +374,7 @@ class PHBase(SPBase):
             self._create_solvers()
         kw = self._solve_kwargs(solver_options)
         t0 = time.perf_counter()
-        self._launch_solve(kw)
+        self._launch_solve(kw, use_scenarios=use_scenarios_not_subproblems)
         nonopt, it_sum, it_max, npol, ncache = self._solve_summary()  # waits for the solve
         dt = time.perf_counter() - t0
         ns = self.n_subproblems
@@ -403,7 +408,7 @@ class PHBase(SPBase):
             status = self.batch.status.cpu().numpy()
             self.scenario_feasible = status <= 1
             sub_names = self.local_scenario_names
-            if self.bundling:  # the reference gripes per subproblem (phbase.py:959-978)
+            if not getattr(self, "_solved_scenarios", True):  # the reference gripes per subproblem (phbase.py:959-978)
                 status = self.bbatch.status.cpu().numpy()
                 sub_names = self.bundle_layout.names
         elif not self._all_feasible:
@@ -415,7 +420,7 @@ class PHBase(SPBase):
         if self.spcomm is not None:
             name = type(self.spcomm).__name__
         why = {2: "primal infeasible (certificate)", 3: "dual infeasible, unbounded (certificate)"}
-        what = "bundle" if self.bundling else "scenario"
+        what = "scenario" if getattr(self, "_solved_scenarios", True) else "bundle"
         # the reference prints one line per infeasible / unbounded solve
         # (phbase.py:959-978); a batch of 10k scenarios prints the first few
         # and a count (all of them with verbose)
@@ -496,8 +501,10 @@ class PHBase(SPBase):
     def Ebound(self, verbose=False, extra_sum_terms=None):
         """phbase.py:314-354: sum over subproblems of probability x
         outer_bound (+ extra terms); a bundle's probability is the sum of its
-        scenarios' (phbase.py:1297-1298)."""
-        if self.bundling:
+        scenarios' (phbase.py:1297-1298).  After a solve_loop over the
+        scenarios themselves (use_scenarios_not_subproblems) the scenarios'
+        bounds."""
+        if not getattr(self, "_solved_scenarios", True):
             bb = self.bbatch
             ob = bb.dbound + bb.const
             ob = (ob if self.is_minimizing else -ob).contiguous()
@@ -530,19 +537,32 @@ class PHBase(SPBase):
 
     # ------------------------------------------- fixed-nonant solves --
     def _save_nonants(self):
-        """phbase.py _save_nonants: the current nonant values of every local
-        scenario (device copy)."""
-        if self.bundling:  # (phbase.py:451-455: not on bundles in the reference either)
-            raise RuntimeError("_save_nonants called for a bundle")
+        """phbase.py:464-486 _save_nonants: the current nonant values of
+        every local scenario (device copy).  With bundles the scenario x
+        holds the bundle solution (scattered back after every bundle solve),
+        so the same copy serves both batches."""
         cols = torch.as_tensor(self.batch_data.nonant_cols.astype(np.int64), device=self.device)
         self._saved_nonant_cols = cols
         self._saved_nonants = self.batch.x.view(self.batch.n, self.S_loc).index_select(0, cols).clone()
 
+    def _bundle_nonant_index(self):
+        """Bundle-batch flat indices of every (nonant slot, scenario) element,
+        [K][S] (the solution scatter's x_idx restricted to the nonant
+        columns)."""
+        if getattr(self, "_b_nonant_idx", None) is None:
+            cols = torch.as_tensor(self.batch_data.nonant_cols.astype(np.int64), device=self.device)
+            S = self.S_loc
+            flat = (cols[:, None] * S + torch.arange(S, device=self.device)[None, :]).reshape(-1)
+            self._b_nonant_idx = self._b_x_idx.to(torch.int64).index_select(0, flat)
+        return self._b_nonant_idx
+
     def _fix_nonants(self, xhat_slots):
-        """phbase.py _fix_nonants: every local scenario's nonants fixed at the
-        node-slot values xhat_slots [G] (l = u on the nonant columns)."""
-        if self.bundling:
-            raise RuntimeError("_fix_nonants called for a bundle")
+        """phbase.py:514-549 _fix_nonants: every local scenario's nonants
+        fixed at the node-slot values xhat_slots [G] (l = u on the nonant
+        columns).  With bundles the reference fixes the scenarios' Vars,
+        which live in the bundle EFs: the same values go to the bundle
+        batch's nonant columns of every block (its solve_loop then solves the
+        bundles with those nonants fixed)."""
         b = self.batch
         n, S = b.n, self.S_loc
         vals = torch.as_tensor(np.asarray(xhat_slots, dtype=np.float64)[self.gid_host],
@@ -555,16 +575,31 @@ class PHBase(SPBase):
         b.set_bounds(l.reshape(-1), u.reshape(-1))
         x = b.x.view(n, S)
         x[cols] = vals   # the warm start sits on the fixed values
+        if self.bundling:
+            bb = self.bbatch
+            idx = self._bundle_nonant_index()
+            v = vals.reshape(-1)
+            bl = bb.l.clone().reshape(-1)
+            bu = bb.u.clone().reshape(-1)
+            bl[idx] = v
+            bu[idx] = v
+            bb.set_bounds(bl, bu)
+            bb.x.view(-1)[idx] = v
 
     def _unfix_nonants(self):
         self.batch.set_bounds(self.batch.l, self.batch.u)
+        if self.bundling:
+            self.bbatch.set_bounds(self.bbatch.l, self.bbatch.u)
 
     def _restore_nonants(self):
-        """phbase.py _restore_nonants: saved nonant values back, bounds freed."""
+        """phbase.py:488-512 _restore_nonants: saved nonant values back,
+        bounds freed (both batches when bundling)."""
         self._unfix_nonants()
         if getattr(self, "_saved_nonants", None) is not None:
             x = self.batch.x.view(self.batch.n, self.S_loc)
             x[self._saved_nonant_cols] = self._saved_nonants
+            if self.bundling:
+                self.bbatch.x.view(-1)[self._bundle_nonant_index()] = self._saved_nonants.reshape(-1)
 
     # ---------------------------------------------------------- W I/O --
     def W_from_flat_list(self, flat_list):
@@ -619,7 +654,7 @@ class PHBase(SPBase):
         for s in range(self.S_loc):
             target = models[s] if models is not None else views[s]
             for key, r in self.rho_setter(target):
-                rho[self._nonant_slot_of(s, key), s] = float(r)
+                rho[self._nonant_slot_of(s, key, "rho_setter"), s] = float(r)
 
     # ----------------------------------------------------------- drivers --
     def Iter0(self):

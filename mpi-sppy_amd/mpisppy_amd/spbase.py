@@ -72,7 +72,7 @@ class SPBase:
         if self.n_proc > len(self.all_scenario_names):
             raise RuntimeError("More ranks than scenarios")
         self.names_in_bundles = None
-        self.bundling = bool(options.get("bundles_per_rank", 0))
+        self.bundling = int(options.get("bundles_per_rank", 0) or 0) > 0  # spbase.py:206 (> 0)
         if "branching_factors" in options:
             self.branching_factors = options["branching_factors"]
         else:
@@ -212,10 +212,11 @@ class SPBase:
         self.gid_host = gid
         self.slot_k_host, self.slot_s0_host, self.slot_s1_host = slot_k, slot_s0, slot_s1
 
-    def _nonant_slot_of(self, s, key):
+    def _nonant_slot_of(self, s, key, who="variable_probability"):
         """Nonant slot k of scenario s named by ``key``: a nonant VarData of
         the scenario's model, ``id()`` of one (the reference's form,
-        ``spbase.py:386-388``), or a nonant variable name."""
+        ``spbase.py:386-388``), or a nonant variable name.  ``who`` names the
+        caller in the error messages (variable_probability, rho_setter)."""
         d = self.batch_data
         if not hasattr(self, "_slot_by_name"):
             names = self.nonant_names()
@@ -223,11 +224,11 @@ class SPBase:
             self._col2slot = {int(c): k for k, c in enumerate(d.nonant_cols)}
         if isinstance(key, str):
             if key not in self._slot_by_name:
-                raise KeyError(f"variable_probability: {key!r} is not a nonant")
+                raise KeyError(f"{who}: {key!r} is not a nonant")
             return self._slot_by_name[key]
         models = d.models
         if models is None:
-            raise TypeError("variable_probability: without per-scenario models, name nonants "
+            raise TypeError(f"{who}: without per-scenario models, name nonants "
                             "by variable name")
         mdl = models[s]
         from . import repn
@@ -240,11 +241,11 @@ class SPBase:
                         ids[id(vd)] = self._col2slot[repn.column_of(mdl, vd)]
                 mdl._mpisppy_amd_nonant_ids = ids
             if key not in ids:
-                raise KeyError("variable_probability: id is not a nonant of the scenario")
+                raise KeyError(f"{who}: id is not a nonant of the scenario")
             return ids[key]
         col = repn.column_of(mdl, key)
         if col not in self._col2slot:
-            raise KeyError("variable_probability: variable is not a nonant")
+            raise KeyError(f"{who}: variable is not a nonant")
         return self._col2slot[col]
 
     def _use_variable_probability_setter(self, verbose=False):

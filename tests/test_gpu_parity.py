@@ -905,6 +905,84 @@ def test_bundled_ph_matches_oracle(model):
     assert _rel(xb, np.array(orc.xbar)) < 1e-5
 
 
+def test_bundled_xhat_matches_oracle():
+    """xhat on a bundled run (phbase.py:464-549 _save/_fix/_restore_nonants
+    loop over the scenarios, whose Vars live in the bundle EFs; xhatbase then
+    solve_loops the bundles with the nonants fixed): the candidate's expected
+    objective equals the oracle's exact restatement and the unbundled run's;
+    the nonants come back unfixed (the next bundle solve moves them), and
+    solve_loop(use_scenarios_not_subproblems=True) solves the scenario batch."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    from mpisppy_amd.extensions.xhatbase import XhatBase
+    from oracle.ph_oracle import xhat_objective
+    names = [f"scen{i}" for i in range(12)]
+    bph = PH(_opts(PHIterLimit=6, convthresh=0.0, bundles_per_rank=4), names, farmer.scenario_creator)
+    bph.ph_main()
+    cols = list(bph.batch_data.nonant_cols)
+    xb = XhatBase(bph)
+    for sname in ("scen0", "scen7"):
+        s = names.index(sname)
+        xn = bph.batch.x.view(bph.batch.n, 12)[cols, s].cpu().numpy()
+        obj = xb._try_one({"ROOT": sname})
+        ref = xhat_objective([om.farmer(nm) for nm in names], {"ROOT": xn})
+        assert obj is not None and abs(obj - ref) / abs(ref) < 1e-7, (sname, obj, ref)
+        S = len(names)
+        xs = bph.batch.x.view(bph.batch.n, S)[cols].cpu().numpy()
+        assert np.allclose(xs, bph._saved_nonants.cpu().numpy())   # nonants restored
+    # the bundles' bounds are back: a bundled solve moves the nonants again
+    bph.solve_loop(solver_options=bph.current_solver_options)
+    assert np.all(bph.bbatch.status.cpu().numpy() == 0)
+    # use_scenarios_not_subproblems: the scenario batch, W and prox as set
+    bph.solve_loop(solver_options=bph.current_solver_options, use_scenarios_not_subproblems=True)
+    assert np.all(bph.batch.status.cpu().numpy() == 0)
+    assert bph.n_subproblems == 12
+    bph.solve_loop(solver_options=bph.current_solver_options)
+    assert bph.n_subproblems == 3
+
+
+def test_async_spokes_with_teams_match_sync():
+    """Hub + Lagrangian + xhat spokes on farmer c=1000 (the big path: three
+    scenarios share the resident grid as teams, whose blocks wait for each
+    other) with the spokes' batches on streams of their own overlapping the
+    hub's kernels: the team and persistent kernels go through cooperative
+    launches (phgpu.hip launch_coop), so two cylinders' team launches cannot
+    hold each other's blocks off the chip.  The run must finish without a
+    device check (PH_EDEV / CHK_BARRIER), and the spokes' bounds at the hub's
+    final state equal those of the same run with blocking spokes."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.phbase import PHBase
+    from mpisppy_amd.cylinders.hub import PHHub
+    from mpisppy_amd.cylinders.lagrangian_bounder import LagrangianOuterBound
+    from mpisppy_amd.cylinders.xhatshufflelooper_bounder import XhatShuffleInnerBound
+    from mpisppy_amd.utils.sputils import spin_the_wheel
+    from mpisppy_amd.examples import farmer
+    names = [f"scen{i}" for i in range(3, 6)]
+    base = dict(scenario_creator=farmer.scenario_creator, all_scenario_names=names,
+                scenario_creator_kwargs={"crops_multiplier": 1000})
+    finals = {}
+    for async_spokes in (True, False):
+        hub_dict = {"hub_class": PHHub, "hub_kwargs": {"options": {"rel_gap": None}, "sync_every": 2,
+                                                       "async_spokes": async_spokes},
+                    "opt_class": PH,
+                    "opt_kwargs": dict(PHoptions=_opts(PHIterLimit=6, convthresh=-1.0), **base)}
+        spokes = [{"spoke_class": LagrangianOuterBound, "opt_class": PHBase,
+                   "opt_kwargs": dict(PHoptions=_opts(PHIterLimit=6), **base)},
+                  {"spoke_class": XhatShuffleInnerBound, "opt_class": PHBase,
+                   "opt_kwargs": dict(PHoptions=_opts(PHIterLimit=6), **base)}]
+        hub, _ = spin_the_wheel(hub_dict, spokes)
+        assert hub.opt._PHIter == 6
+        finals[async_spokes] = [sp.hub_sync(hub.opt) for sp in hub.spokes] + [hub.opt.Eobjective()]
+    a, s = finals[True], finals[False]
+    assert abs(a[0] - s[0]) <= 1e-7 * abs(s[0]), (a, s)    # Lagrangian bound at the final W
+    assert abs(a[2] - s[2]) <= 1e-9 * abs(s[2]), (a, s)    # the hub's trajectory is the same
+    # (the xhat spoke's best so far depends on which hub nonants each
+    # candidate saw -- lagged by a sync when asynchronous): both are inner
+    # bounds above the Lagrangian one
+    assert a[1] is not None and s[1] is not None
+    assert min(a[1], s[1]) >= s[0] * (1 - 1e-9) if s[0] > 0 else min(a[1], s[1]) >= s[0] * (1 + 1e-9)
+
+
 def test_wxbar_files_from_the_hip_path_match_oracle_and_resume(tmp_path):
     """SURVEY 8 f-3 on the HIP path (utils/wxbarutils.py:40-79, 264-284 via
     the WXBarWriter / WXBarReader extensions): a GPU PH on farmer S=12 writes
