@@ -44,7 +44,10 @@ struct KktSymbolic {
 
   // Minimum-degree order on the KKT graph (explicit elimination graph,
   // ties by vertex index: deterministic), then the symbolic factorisation.
-  bool analyze(int n_, int m_, const int32_t *row_ptr, const int32_t *col_idx) {
+  // lists = false: no update lists (ecp / ec1 / ec2 / eck stay empty; the
+  // supernodal factorisation of kkt_super.h needs only the order and L's
+  // pattern), ncontrib is still counted.
+  bool analyze(int n_, int m_, const int32_t *row_ptr, const int32_t *col_idx, bool lists = true) {
     n = n_;
     m = m_;
     N = n + m;
@@ -161,10 +164,11 @@ struct KktSymbolic {
         error = "the KKT factor has more than 2^31 entries";
         return false;
       }
-      if (nc > kMaxContrib) {
+      if (lists && nc > kMaxContrib) {
         error = "the KKT factor's update lists exceed 2^28 entries";
         return false;
       }
+      ncontrib = (long)nc;
     }
     Lcp.assign(N + 1, 0);
     for (int c = 0; c < N; ++c) Lcp[c + 1] = Lcp[c] + (int)pat[c].size();
@@ -220,12 +224,17 @@ struct KktSymbolic {
         error = "the level-order renumbering failed";
         return false;
       }
-    // ---- update lists: entry (r,c) -= L(r,k) D(k) L(c,k) for k < c
-    std::vector<int32_t> cnt(nnzL + 1, 0);
     auto entry = [&](int r, int c) {
       const auto b = Lri.begin() + Lcp[c], e = Lri.begin() + Lcp[c + 1];
       return (int32_t)(std::lower_bound(b, e, r) - Lri.begin());
     };
+    ecp.clear();
+    ec1.clear();
+    ec2.clear();
+    eck.clear();
+    if (lists) {
+    // ---- update lists: entry (r,c) -= L(r,k) D(k) L(c,k) for k < c
+    std::vector<int32_t> cnt(nnzL + 1, 0);
     for (int k = 0; k < N; ++k)
       for (int a = Lcp[k]; a < Lcp[k + 1]; ++a)
         for (int b = a + 1; b < Lcp[k + 1]; ++b) cnt[entry(Lri[b], Lri[a]) + 1]++;
@@ -246,6 +255,7 @@ struct KktSymbolic {
             ec2[q] = a;  // L(c,k)
             eck[q] = k;
           }
+    }
     }
     // ---- A's entries in L
     apos.resize(nnz);

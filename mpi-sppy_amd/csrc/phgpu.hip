@@ -27,6 +27,7 @@
 
 #include "../../include/phgpu.h"
 #include "kkt_symbolic.h"
+#include "kkt_super.h"
 
 #define PHGPU_VERSION "phgpu 0.1 gfx950"
 
@@ -2160,6 +2161,7 @@ __global__ void __launch_bounds__(1024) loop_conv_local_kernel(
 }
 
 #include "solve_mid.inc"
+#include "solve_super.inc"
 #include "solve_big.inc"
 
 // ------------------------------------------------------------------------
@@ -3496,6 +3498,8 @@ struct ph_batch {
   KktSymbolic sym;
   int32_t *d_sym = nullptr;   // every int32 array of the symbolic analysis + tails
   uint16_t *d_sym16 = nullptr;  // the uint16 index arrays the mid polish stages in LDS
+  int32_t *d_ssym = nullptr;    // the supernodal analysis' arrays (kkt_super.h; big path, bg.sd)
+  size_t big_plds_bytes = 0;    // LDS of big_polish_kernel (BIG_SMALL_LDS, or + the supernodal pool)
   MidArgs md{};
   int mid_lds_doubles = 0;    // LDS carve of solve_mid (doubles)
   size_t mid_lds_bytes = 0;   // LDS of the PDHG phase kernel
@@ -3757,6 +3761,61 @@ static int kkt_knobs(ph_batch *b) {
 // LDS plan of the mid-size path; uploads the index arrays (one buffer).
 static int big_init(ph_batch *b);
 
+// The supernodal analysis of the big path's KKT pattern (kkt_super.h) and
+// its device arrays (bg.sd); the polish's factor then holds panels (kd.nnzL
+// = their total), kd.pos / kd.apos map into the supernodal numbering.
+static constexpr long SUPER_MIN_CONTRIB = 4L << 20;
+
+static int super_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx) {
+  KktSuper sp;
+  if (!sp.build(b->sym, row_ptr, col_idx))
+    return fail(PH_EINVAL, std::string("ph_batch_create: supernodal analysis refused the pattern: ") +
+                               (sp.error ? sp.error : "?"));
+  if (sp.max_f > SUPER_SLICE) return fail(PH_EINVAL, "ph_batch_create: a supernodal front exceeds the LDS slice");
+  const std::vector<const std::vector<int32_t> *> parts = {
+      &sp.pos, &sp.sfirst, &sp.sw, &sp.sr, &sp.poff, &sp.uoff, &sp.voff, &sp.srp, &sp.srow, &sp.rel, &sp.chp,
+      &sp.chl, &sp.kpre, &sp.lvi, &sp.itg, &sp.itp, &sp.itsn, &sp.lvr, &sp.rdp, &sp.rsn, &sp.rlo, &sp.lvb,
+      &sp.lbs, &sp.apos};
+  std::vector<size_t> off;
+  std::vector<int32_t> all;
+  for (auto *v : parts) {
+    off.push_back(all.size());
+    all.insert(all.end(), v->begin(), v->end());
+    all.resize((all.size() + 3) & ~size_t(3), 0);
+  }
+  if (int rc = dalloc(&b->d_ssym, all.size())) return rc;
+  HIP_OK(hipMemcpy(b->d_ssym, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  const int32_t *d = b->d_ssym;
+  KsDev &k = b->bg.sd;
+  k = KsDev{};
+  k.on = 1;
+  k.ns = sp.ns;
+  k.nlev = sp.nlev;
+  k.u_total = sp.u_total;
+  k.v_total = sp.v_total;
+  k.lds_base = (MAX_WAVES * 10 + 2 + 7) & ~7;
+  int q = 0;
+  k.pos = d + off[q++]; k.sfirst = d + off[q++]; k.sw = d + off[q++]; k.sr = d + off[q++];
+  k.poff = d + off[q++]; k.uoff = d + off[q++]; k.voff = d + off[q++];
+  k.srp = d + off[q++]; k.srow = d + off[q++]; k.rel = d + off[q++];
+  k.chp = d + off[q++]; k.chl = d + off[q++]; k.kpre = d + off[q++];
+  k.lvi = d + off[q++]; k.itg = d + off[q++]; k.itp = d + off[q++]; k.itsn = d + off[q++];
+  k.lvr = d + off[q++]; k.rdp = d + off[q++]; k.rsn = d + off[q++]; k.rlo = d + off[q++];
+  k.lvb = d + off[q++]; k.lbs = d + off[q++];
+  const int32_t *apos = d + off[q++];
+  KktDev &kd = b->md.kd;
+  kd.pos = k.pos;
+  kd.apos = apos;
+  kd.nnzL = (int)sp.panel_total;
+  if (const char *v = std::getenv("PHGPU_VERBOSE"); v && std::atoi(v) != 0)
+    std::fprintf(stderr,
+                 "phgpu super: N %d supernodes %d levels %d panels %ld U %ld V %ld doubles, flops %ld, "
+                 "max front %d, big %d (%zu rounds), small items %zu; per-entry form: %ld contributions\n",
+                 sp.N, sp.ns, sp.nlev, sp.panel_total, sp.u_total, sp.v_total, sp.flops, sp.max_f, sp.nbig,
+                 sp.rdp.size() - 1, sp.itg.size(), (long)b->sym.ncontrib);
+  return PH_OK;
+}
+
 // Scenarios beyond the mid-size plan (max(n, m) > 3072) take the big path
 // (solve_big.inc): the same analysis, long-line lists instead of tails, the
 // state in HBM workspace slices.
@@ -3765,9 +3824,24 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   // PHGPU_FORCE_BIG=1: measurement hook, the big path for a mid-size shape
   const char *fb = std::getenv("PHGPU_FORCE_BIG");
   bool big = (fb && std::atoi(fb) != 0) || !pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr);
-  if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx))
+  // the big path's LDL' is supernodal (kkt_super.h, solve_super.inc) past
+  // SUPER_MIN_CONTRIB update contributions of the per-entry form (UC: 58M;
+  // F4: per-entry); PHGPU_KKT_SUPER=1 / 0 forces it on / off (parity tests,
+  // measurement).  A big pattern's analysis first counts the contributions
+  // without building the per-entry update lists.
+  const char *se = std::getenv("PHGPU_KKT_SUPER");
+  const int super_env = se && *se ? std::atoi(se) : -1;
+  bool lists = !big;
+  if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx, lists))
     return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
                                (b->sym.error ? b->sym.error : "?"));
+  bool use_super = big && (super_env == 1 || (super_env != 0 && b->sym.ncontrib > SUPER_MIN_CONTRIB));
+  if (big && !use_super) {
+    lists = true;
+    if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx, true))
+      return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
+                                 (b->sym.error ? b->sym.error : "?"));
+  }
   const KktSymbolic &y = b->sym;
   auto up2 = [](long v) { return (v + 1) & ~1L; };
   auto up4 = [](long v) { return (v + 3) & ~3L; };
@@ -3807,7 +3881,10 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     // uint16 or do not fit (even with the workspace in HBM) takes the big path
     const long fixed = (common + up2(b->nnz) + 2) * 8 + len16 * 2;
     ws_lds = fixed + ws * 8 <= 160 * 1024;
-    if (!fit16 || fixed > 160 * 1024) big = true;
+    if (!fit16 || fixed > 160 * 1024) {
+      big = true;
+      use_super = super_env == 1 || (super_env != 0 && b->sym.ncontrib > SUPER_MIN_CONTRIB);
+    }
   }
   if (big) {
     b->mblock = BIG_BLOCK;
@@ -3874,7 +3951,18 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     b->big_lds_bytes = sizeof(double) * ((size_t)MAX_WAVES * 10 + 2 + up2(b->m));
     b->big_ylds = b->big_lds_bytes <= 160 * 1024;
     if (!b->big_ylds) b->big_lds_bytes = BIG_SMALL_LDS;  // y in the workspace slice
-    g.ws_stride = std::max({big_pdhg_ws_len(b->n, b->m), big_pol_ws_len(b->n, b->m, y.nnzL, y.N),
+    b->big_plds_bytes = BIG_SMALL_LDS;
+    g.sd = KsDev{};
+    long ut = 0, vt = 0;
+    int nnzL_ws = y.nnzL;
+    if (use_super) {
+      if (int rc = super_setup(b, row_ptr, col_idx)) return rc;
+      ut = g.sd.u_total;
+      vt = g.sd.v_total;
+      nnzL_ws = kd.nnzL;  // the panels
+      b->big_plds_bytes = sizeof(double) * ((size_t)g.sd.lds_base + SUPER_POOL);
+    }
+    g.ws_stride = std::max({big_pdhg_ws_len(b->n, b->m), big_pol_ws_len(b->n, b->m, nnzL_ws, y.N, ut, vt),
                             2 * up2(b->n) + up2(b->m)});
     b->big = true;
     b->mid_ready = false;
@@ -4281,8 +4369,10 @@ static int big_init(ph_batch *b) {
   } else {
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, big_kernel<false>, BIG_BLOCK, b->big_lds_bytes));
   }
+  HIP_OK(hipFuncSetAttribute((const void *)big_polish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)b->big_plds_bytes));
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, big_polish_kernel, BIG_BLOCK,
-                                                      BIG_SMALL_LDS));
+                                                      b->big_plds_bytes));
   if (per_cu < 1 || per_cu_p < 1) return fail(PH_EINVAL, "ph_batch_bind: the big-path kernels cannot be resident");
   int grid = std::min(b->S, std::min(per_cu, per_cu_p) * std::max(1, cus));
   if (const int cap = mid_grid_cap()) grid = std::min(grid, cap);
@@ -4393,7 +4483,7 @@ static long big_polish_max_contrib() {
 
 static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   a.polish = opts ? opts->polish : 1;
-  if (b->big && b->sym.ncontrib > big_polish_max_contrib()) a.polish = 0;
+  if (b->big && !b->bg.sd.on && b->sym.ncontrib > big_polish_max_contrib()) a.polish = 0;
   a.cache = nullptr;
   a.wl = nullptr;
   if (int rc = mid_init(b)) return rc;
@@ -4477,7 +4567,7 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode, 0, 0};
     if (int rc = phase_event(b, 1)) return rc;
     if (b->big) {
-      hipLaunchKernelGGL(big_polish_kernel, dim3(b->big_grid), dim3(BIG_BLOCK), BIG_SMALL_LDS, b->stream,
+      hipLaunchKernelGGL(big_polish_kernel, dim3(b->big_grid), dim3(BIG_BLOCK), b->big_plds_bytes, b->stream,
                          a, b->md, b->bg, ph);
       HIP_OK(hipGetLastError());
       return phase_event(b, -1);
@@ -5314,7 +5404,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
-                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
+                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ssym, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
                   b->d_bws, b->d_lpart, b->d_lbar, b->d_teambar, b->d_teampart,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)

@@ -55,6 +55,25 @@ b = ph.batch
 torch.cuda.synchronize()
 say(f"built n={b.n} m={b.m} nnz={b.nnz} K={b.K}")
 b.set_timing(True)
+import ctypes  # noqa: E402
+_lib = b.lib
+_lib.ph_debug_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+_lib.ph_debug_prof.restype = ctypes.c_int32
+_prof = np.zeros(64, dtype=np.int64)
+
+
+def prof_reset():
+    _lib.ph_debug_prof(b.handle, 1, None)
+
+
+def prof_read(tag):
+    _lib.ph_debug_prof(b.handle, 1, _prof.ctypes.data)
+    p = _prof
+    say(f"  {tag} polish counters: polishes {p[9]} rounds {p[10]} solves {p[11]} accepted {p[12]}; "
+        f"no change {p[1]} non-finite {p[2]} round limit {p[3]} refine short {p[4]} fail ep/ed/eg {p[6]}/{p[7]}/{p[8]}")
+
+
+prof_reset()
 t = time.perf_counter()
 tb = ph.Iter0()
 torch.cuda.synchronize()
@@ -69,6 +88,7 @@ print("  final errors of the first scenarios:", d[:3, :3], flush=True)
 nt, _, _, _, nk, k_ms, np_, p_ms = b.read_timing_full()
 say(f"  big_kernel {nk} launches {k_ms:.1f} ms, polish {np_} launches {p_ms:.1f} ms; "
     f"{k_ms / max(it.sum() / S, 1):.4f} ms per PDHG step (per scenario, in parallel)")
+prof_read("Iter0")
 if S <= 8:
     from oracle import models as om
     from oracle.solve import _highs_solve
@@ -80,6 +100,7 @@ if S <= 8:
     ob = (b.dbound.cpu().numpy() + b.const.cpu().numpy())[:3]
     say(f"oracle LP values {vals}; GPU outer bounds {ob.tolist()}; rel {(ob - vals) / np.abs(vals)}")
 for k in range(NIT):
+    prof_reset()
     t = time.perf_counter()
     ph.Compute_Xbar()
     ph.Update_W(False)
@@ -90,3 +111,6 @@ for k in range(NIT):
     d = b.diagnostics()
     say(f"PH iteration {k + 1}: {1000 * (time.perf_counter() - t):.1f} ms, statuses {np.bincount(st, minlength=4)}, "
         f"PDHG steps mean {it.mean():.0f} max {it.max()}, how {np.bincount(d[:, 4].astype(int), minlength=4)}")
+    nt, _, _, _, nk, k_ms, np_, p_ms = b.read_timing_full()
+    say(f"  big_kernel {nk} launches {k_ms:.1f} ms, polish {np_} launches {p_ms:.1f} ms")
+    prof_read(f"PH {k + 1}")
