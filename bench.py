@@ -123,7 +123,7 @@ def cpu_baseline(c, scens, convthresh, cores=16, f3_crops=100, f3_sample=64, f3_
     sample for the F3 companion config."""
     sys.path.insert(0, ROOT)
     from oracle import ph_dist
-    cores = max(1, min(cores, len(os.sched_getaffinity(0))))
+    cores = job_cpus() if cores <= 0 else max(1, min(cores, len(os.sched_getaffinity(0))))
     t0 = time.perf_counter()
     r = ph_dist.run(cores, scens, crops=c, rho=1.0, convthresh=convthresh)
     wall = time.perf_counter() - t0
@@ -158,11 +158,36 @@ def cpu_baseline(c, scens, convthresh, cores=16, f3_crops=100, f3_sample=64, f3_
     return out
 
 
+def cgroup_cpu_quota():
+    """CPUs this job may use by its cgroup (cpu.max quota / period), or None
+    when unlimited or unreadable.  The GPU box's job cgroup allows 16 CPUs of
+    its 2 x 64-core host (cpu.max "1600000 100000"), so more gloo ranks than
+    that would only time-slice the same 16 CPUs."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q == "max":
+            return None
+        return max(1, int(int(q) // int(per)))
+    except Exception:
+        return None
+
+
+def job_cpus():
+    """The CPUs available to this job: the affinity mask capped by the
+    cgroup quota (SURVEY 8(d)'s "all cores" of the host, as far as the job
+    may use them)."""
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpu_quota()
+    return min(n, q) if q else n
+
+
 def host_cpu_info():
     """lscpu of the host the CPU baseline ran on (record N and
     lscpu) and the CPUs this process may use."""
     import subprocess
-    info = {"affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    info = {"affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+            "cgroup_cpu_quota": cgroup_cpu_quota()}
     try:
         txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         keep = ("Model name", "CPU(s)", "Thread(s) per core", "Core(s) per socket", "Socket(s)",
@@ -174,6 +199,25 @@ def host_cpu_info():
     except Exception as e:  # lscpu missing: say so
         info["lscpu_error"] = repr(e)
     return info
+
+
+def vs_cpu(gpu_tol, cpu):
+    """The like-for-like GPU / CPU comparison: PH from Iter0 to convthresh on
+    the SAME farmer instance (cpu_baseline's sample size), wall seconds on
+    the CPU baseline's ranks over the GPU's; and the subproblem solve rates of
+    those two runs."""
+    if not gpu_tol or not cpu or not cpu.get("ph_to_tol") or not gpu_tol.get("seconds"):
+        return None
+    c = cpu["ph_to_tol"]
+    g_solves = gpu_tol["scenarios"] * (gpu_tol["ph_iterations"] + 1)
+    return {"ph_to_tol_speedup": round(c["seconds"] / gpu_tol["seconds"], 1),
+            "solves_per_s_ratio": round(g_solves / gpu_tol["seconds"] / cpu["value"], 1),
+            "gpu_seconds": gpu_tol["seconds"], "cpu_seconds": c["seconds"], "cpu_cores": cpu["cores"],
+            "scenarios": gpu_tol["scenarios"],
+            "same_iterations": gpu_tol["ph_iterations"] == c["ph_iterations"],
+            "basis": "PH wall-clock from Iter0 to convthresh on the same instance: the oracle PH (exact "
+                     "HiGHS subproblem solves, no Pyomo overhead) on cpu_cores gloo ranks of the GPU "
+                     "box's host against one MI355X"}
 
 
 def workload_tag(kind, S_loc, c=None):
@@ -611,7 +655,7 @@ def _parser():
     ap.add_argument("--convthresh", type=float, default=1e-4)
     ap.add_argument("--cpu-scens", type=int, default=200,
                     help="scenarios of the CPU-baseline oracle PH run (and of the GPU run beside it)")
-    ap.add_argument("--cpu-cores", type=int, default=16,
+    ap.add_argument("--cpu-cores", type=int, default=0,
                     help="CPU-baseline processes (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hbm-crops", type=int, default=100,
@@ -871,12 +915,9 @@ def run():
             "ms_per_step": round(dt / args.steps * 1000.0, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (round(value / cpu["value"], 1) if cpu and cpu.get("value") else None),
-            "vs_baseline_basis": "value / cpu_baseline.value: the oracle PH (exact HiGHS subproblem "
-                                 "solves, no Pyomo overhead) on the GPU box's host, cpu_baseline.cores "
-                                 "gloo ranks, a 200-scenario sample of the same farmer workload "
-                                 "(BASELINE.md section 2's CPU baseline; the reference publishes no "
-                                 "number for this metric)",
+            # (BASELINE.md holds no published number for this metric)
+            "vs_baseline": None,
+            "vs_cpu": vs_cpu(tol_small, cpu),
             "dtype": "f64",
             "data": "synthetic (reference farmer generator, examples/farmer/farmer.py)",
             "config": {"workload": f"farmer PH, {S} scenarios ({args.scens} per GPU), crops_multiplier={c} "

@@ -66,6 +66,9 @@ struct KktSuper {
   // rsn[rdp..] with their LDS offsets rlo), big supernodes by level (lvb /
   // lbs: the solve deals them to waves)
   std::vector<int32_t> kpre, lvi, itg, itp, itsn, lvr, rdp, rsn, rlo, lvb, lbs;
+  // per supernode the device's record, three int4: {first, w, r, poff},
+  // {uoff, voff, first child (chl), children}, {srp, kpre, level, 0}
+  std::vector<int32_t> rec;
 
   static constexpr int kPool = 16 * 1024;  // doubles of the device's LDS pool (SUPER_POOL)
   // lane-group size of a small front (8 .. 64 lanes, one front row each)
@@ -398,6 +401,21 @@ struct KktSuper {
         rdp.push_back((int32_t)rsn.size());
       }
       lvr[l + 1] = (int32_t)(rdp.size() - 1);
+    }
+    rec.assign((size_t)ns * 12, 0);
+    for (int t = 0; t < ns; ++t) {
+      int32_t *q = rec.data() + (size_t)t * 12;
+      q[0] = sfirst[t];
+      q[1] = sw[t];
+      q[2] = sr[t];
+      q[3] = poff[t];
+      q[4] = uoff[t];
+      q[5] = voff[t];
+      q[6] = chp[t];
+      q[7] = chp[t + 1] - chp[t];
+      q[8] = srp[t];
+      q[9] = kpre[t];
+      q[10] = lev[t];
     }
     // A's entries: the panel offset of the lower KKT entry (max, min)
     const int nnz = row_ptr[m];

@@ -3498,7 +3498,9 @@ struct ph_batch {
   KktSymbolic sym;
   int32_t *d_sym = nullptr;   // every int32 array of the symbolic analysis + tails
   uint16_t *d_sym16 = nullptr;  // the uint16 index arrays the mid polish stages in LDS
-  int32_t *d_ssym = nullptr;    // the supernodal analysis' arrays (kkt_super.h; big path, bg.sd)
+  int32_t *d_ssym = nullptr;    // the supernodal analysis' arrays (kkt_super.h; big path, bg.sdp)
+  double *d_ksdev = nullptr;    // the KsDev struct of those arrays (device memory)
+  int sd_lds_base = 0;
   size_t big_plds_bytes = 0;    // LDS of big_polish_kernel (BIG_SMALL_LDS, or + the supernodal pool)
   MidArgs md{};
   int mid_lds_doubles = 0;    // LDS carve of solve_mid (doubles)
@@ -3764,8 +3766,6 @@ static int big_init(ph_batch *b);
 // The supernodal analysis of the big path's KKT pattern (kkt_super.h) and
 // its device arrays (bg.sd); the polish's factor then holds panels (kd.nnzL
 // = their total), kd.pos / kd.apos map into the supernodal numbering.
-static constexpr long SUPER_MIN_CONTRIB = 4L << 20;
-
 static int super_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx) {
   KktSuper sp;
   if (!sp.build(b->sym, row_ptr, col_idx))
@@ -3773,21 +3773,19 @@ static int super_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_i
                                (sp.error ? sp.error : "?"));
   if (sp.max_f > SUPER_SLICE) return fail(PH_EINVAL, "ph_batch_create: a supernodal front exceeds the LDS slice");
   const std::vector<const std::vector<int32_t> *> parts = {
-      &sp.pos, &sp.sfirst, &sp.sw, &sp.sr, &sp.poff, &sp.uoff, &sp.voff, &sp.srp, &sp.srow, &sp.rel, &sp.chp,
-      &sp.chl, &sp.kpre, &sp.lvi, &sp.itg, &sp.itp, &sp.itsn, &sp.lvr, &sp.rdp, &sp.rsn, &sp.rlo, &sp.lvb,
-      &sp.lbs, &sp.apos};
+      &sp.pos, &sp.rec, &sp.srow, &sp.rel, &sp.chl, &sp.lvi, &sp.itg, &sp.itp, &sp.itsn,
+      &sp.lvr, &sp.rdp, &sp.rsn, &sp.rlo, &sp.lvb, &sp.lbs, &sp.apos};
   std::vector<size_t> off;
   std::vector<int32_t> all;
   for (auto *v : parts) {
     off.push_back(all.size());
     all.insert(all.end(), v->begin(), v->end());
-    all.resize((all.size() + 3) & ~size_t(3), 0);
+    all.resize((all.size() + 3) & ~size_t(3), 0);  // (16-byte aligned: rec is read as int4)
   }
   if (int rc = dalloc(&b->d_ssym, all.size())) return rc;
   HIP_OK(hipMemcpy(b->d_ssym, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   const int32_t *d = b->d_ssym;
-  KsDev &k = b->bg.sd;
-  k = KsDev{};
+  KsDev k{};
   k.on = 1;
   k.ns = sp.ns;
   k.nlev = sp.nlev;
@@ -3795,14 +3793,22 @@ static int super_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_i
   k.v_total = sp.v_total;
   k.lds_base = (MAX_WAVES * 10 + 2 + 7) & ~7;
   int q = 0;
-  k.pos = d + off[q++]; k.sfirst = d + off[q++]; k.sw = d + off[q++]; k.sr = d + off[q++];
-  k.poff = d + off[q++]; k.uoff = d + off[q++]; k.voff = d + off[q++];
-  k.srp = d + off[q++]; k.srow = d + off[q++]; k.rel = d + off[q++];
-  k.chp = d + off[q++]; k.chl = d + off[q++]; k.kpre = d + off[q++];
+  k.pos = d + off[q++];
+  k.rec = (const int4 *)(d + off[q++]);
+  k.srow = d + off[q++]; k.rel = d + off[q++]; k.chl = d + off[q++];
   k.lvi = d + off[q++]; k.itg = d + off[q++]; k.itp = d + off[q++]; k.itsn = d + off[q++];
   k.lvr = d + off[q++]; k.rdp = d + off[q++]; k.rsn = d + off[q++]; k.rlo = d + off[q++];
   k.lvb = d + off[q++]; k.lbs = d + off[q++];
   const int32_t *apos = d + off[q++];
+  // the struct itself in device memory (solve_super.inc reads it through a
+  // uniform pointer)
+  if (int rc = dalloc(&b->d_ksdev, (sizeof(KsDev) + 7) / 8)) return rc;
+  HIP_OK(hipMemcpy(b->d_ksdev, &k, sizeof(KsDev), hipMemcpyHostToDevice));
+  b->bg.sdp = (const KsDev *)b->d_ksdev;
+  b->bg.sd_on = 1;
+  b->bg.sd_ut = k.u_total;
+  b->bg.sd_vt = k.v_total;
+  b->sd_lds_base = k.lds_base;
   KktDev &kd = b->md.kd;
   kd.pos = k.pos;
   kd.apos = apos;
@@ -3824,18 +3830,22 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   // PHGPU_FORCE_BIG=1: measurement hook, the big path for a mid-size shape
   const char *fb = std::getenv("PHGPU_FORCE_BIG");
   bool big = (fb && std::atoi(fb) != 0) || !pick_mid(b->n, b->m, &b->mblock, &b->mpc, &b->mpr);
-  // the big path's LDL' is supernodal (kkt_super.h, solve_super.inc) past
-  // SUPER_MIN_CONTRIB update contributions of the per-entry form (UC: 58M;
-  // F4: per-entry); PHGPU_KKT_SUPER=1 / 0 forces it on / off (parity tests,
-  // measurement).  A big pattern's analysis first counts the contributions
-  // without building the per-entry update lists.
+  // the big path's LDL' can be supernodal (kkt_super.h, solve_super.inc):
+  // PHGPU_KKT_SUPER=1 turns it on (its factorisation is parity-tested on F4
+  // and checked against the sparse KKT on UC's pattern).  It is not the
+  // default for UC, the pattern it was built for: the active-set polish
+  // does not finish UC's degenerate LP relaxation from PDHG points (GPU: 0
+  // of 10 Iter0 polishes, tools/uc_probe.py; CPU: tools/uc_polish_lab.py), so
+  // UC solves by PDHG alone (the per-entry form's size limit below) until
+  // the polish does.  A big pattern's analysis first counts the per-entry
+  // form's update contributions without building its lists.
   const char *se = std::getenv("PHGPU_KKT_SUPER");
   const int super_env = se && *se ? std::atoi(se) : -1;
   bool lists = !big;
   if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx, lists))
     return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
                                (b->sym.error ? b->sym.error : "?"));
-  bool use_super = big && (super_env == 1 || (super_env != 0 && b->sym.ncontrib > SUPER_MIN_CONTRIB));
+  bool use_super = big && super_env == 1;
   if (big && !use_super) {
     lists = true;
     if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx, true))
@@ -3883,7 +3893,7 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     ws_lds = fixed + ws * 8 <= 160 * 1024;
     if (!fit16 || fixed > 160 * 1024) {
       big = true;
-      use_super = super_env == 1 || (super_env != 0 && b->sym.ncontrib > SUPER_MIN_CONTRIB);
+      use_super = super_env == 1;
     }
   }
   if (big) {
@@ -3952,15 +3962,17 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
     b->big_ylds = b->big_lds_bytes <= 160 * 1024;
     if (!b->big_ylds) b->big_lds_bytes = BIG_SMALL_LDS;  // y in the workspace slice
     b->big_plds_bytes = BIG_SMALL_LDS;
-    g.sd = KsDev{};
+    g.sdp = nullptr;
+    g.sd_on = 0;
+    g.sd_ut = g.sd_vt = 0;
     long ut = 0, vt = 0;
     int nnzL_ws = y.nnzL;
     if (use_super) {
       if (int rc = super_setup(b, row_ptr, col_idx)) return rc;
-      ut = g.sd.u_total;
-      vt = g.sd.v_total;
+      ut = g.sd_ut;
+      vt = g.sd_vt;
       nnzL_ws = kd.nnzL;  // the panels
-      b->big_plds_bytes = sizeof(double) * ((size_t)g.sd.lds_base + SUPER_POOL);
+      b->big_plds_bytes = sizeof(double) * ((size_t)b->sd_lds_base + SUPER_POOL);
     }
     g.ws_stride = std::max({big_pdhg_ws_len(b->n, b->m), big_pol_ws_len(b->n, b->m, nnzL_ws, y.N, ut, vt),
                             2 * up2(b->n) + up2(b->m)});
@@ -4483,7 +4495,7 @@ static long big_polish_max_contrib() {
 
 static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   a.polish = opts ? opts->polish : 1;
-  if (b->big && !b->bg.sd.on && b->sym.ncontrib > big_polish_max_contrib()) a.polish = 0;
+  if (b->big && !b->bg.sd_on && b->sym.ncontrib > big_polish_max_contrib()) a.polish = 0;
   a.cache = nullptr;
   a.wl = nullptr;
   if (int rc = mid_init(b)) return rc;
@@ -5404,7 +5416,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
-                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ssym, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
+                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ssym, b->d_ksdev, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
                   b->d_bws, b->d_lpart, b->d_lbar, b->d_teambar, b->d_teampart,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)

@@ -1,4 +1,5 @@
 """GPU parity: the HIP batched PH path against the CPU oracle (run with -m gpu)."""
+import sys
 import numpy as np
 import scipy.sparse as sp
 import pytest
@@ -839,12 +840,16 @@ def test_farmer_c1000_big_path_matches_oracle(monkeypatch):
     assert abs(ph2.Eobjective() - eobj_host) <= 1e-9 * abs(eobj_host)
 
 
-def test_farmer_c1000_hard_iter0_lps_match_oracle():
+@pytest.mark.parametrize("super_kkt", ["0", "1"])
+def test_farmer_c1000_hard_iter0_lps_match_oracle(super_kkt, monkeypatch):
     """F4's Iter0 LPs that round 3 left to PDHG (scen22 reached the 200,000
     step limit: the PDHG stalls at a 1e-6 gap on a near-tie between growing
     and buying one crop's feed) now finish through the big path's ratio-test
     polish (solve_big.inc, polish_big): every status optimal, the trivial
-    bound to 1e-7 and the nonants to 1e-6 against the oracle's simplex."""
+    bound to 1e-7 and the nonants to 1e-6 against the oracle's simplex.
+    super_kkt=1: the same with the supernodal factorisation
+    (PHGPU_KKT_SUPER=1, solve_super.inc) in the polish."""
+    monkeypatch.setenv("PHGPU_KKT_SUPER", super_kkt)
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     names = ["scen22", "scen7", "scen41", "scen3"]
@@ -1190,3 +1195,28 @@ def test_big_teams_match_one_block(monkeypatch):
     assert abs(t1 - t0) <= 1e-9 * abs(t0)
     assert abs(e1 - e0) <= 1e-9 * abs(e0)
     assert _rel(x1b, x0b) < 1e-6
+
+
+@pytest.mark.parametrize("kind", ["uc", "farmer1000", "sslp"])
+def test_supernodal_factor_on_device_matches_sparse_kkt(kind, tmp_path):
+    """The supernodal LDL' of the big path (PHGPU_KKT_SUPER=1: kkt_super.h,
+    solve_super.inc) run by one workgroup on a random quasi-definite KKT
+    system of an active set on the workload's pattern (UC's LP relaxation:
+    N = 126,771): the device factor equals the CPU replay of the same
+    algorithm to 1e-9 (every supernode's L, D and update matrix), and the
+    device solve's residual against the sparse K is rounding error.  The
+    test program is built by __graft_entry__.build()."""
+    import json
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "native", "bin", "super_gpu_check")
+    assert os.path.exists(exe), "build() compiles tests/native/bin/super_gpu_check"
+    pat = subprocess.run([sys.executable, os.path.join(root, "tools", "dump_pattern.py"), kind,
+                          "1", "0.2", "0.3", "0.5"], capture_output=True, text=True, check=True).stdout
+    out = subprocess.run([exe], input=pat, capture_output=True, text=True, check=True, timeout=120).stdout
+    lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+    assert any(d.get("factor_match") for d in lines), lines[0]
+    d = lines[-1]
+    assert d["residual"] <= 1e-11 * max(1.0, d["znorm"]), d
+    assert d["rerun_diff"] == 0.0, d   # deterministic
