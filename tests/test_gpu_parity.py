@@ -943,7 +943,7 @@ def test_bundled_xhat_matches_oracle():
     assert np.all(bph.batch.status.cpu().numpy() == 0)
     assert bph.n_subproblems == 12
     bph.solve_loop(solver_options=bph.current_solver_options)
-    assert bph.n_subproblems == 3
+    assert bph.n_subproblems == 4
 
 
 def test_async_spokes_with_teams_match_sync():

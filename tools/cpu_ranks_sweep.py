@@ -17,14 +17,21 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from oracle import ph_dist  # noqa: E402
 
-limit = int(sys.argv[1])
-out = {"host": bench.host_cpu_info(), "job_cpus": bench.job_cpus(), "limit": limit, "scenarios": 200, "runs": []}
-for n in map(int, sys.argv[2:]):
-    t0 = time.perf_counter()
-    r = ph_dist.run(n, 200, crops=1, rho=1.0, convthresh=1e-4, limit=limit)
-    wall = time.perf_counter() - t0
-    out["runs"].append({"ranks": n, "solves": r["subproblem_solves"], "seconds": round(r["seconds_to_tol"], 3),
-                        "solves_per_s": round(r["subproblem_solves"] / r["seconds_to_tol"], 1),
-                        "iterations": r["iterations"], "wall_with_startup": round(wall, 1)})
-    print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
-print(json.dumps(out, indent=1))
+
+def main():
+    limit = int(sys.argv[1])
+    out = {"host": bench.host_cpu_info(), "job_cpus": bench.job_cpus(), "limit": limit, "scenarios": 200, "runs": []}
+    for n in map(int, sys.argv[2:]):
+        t0 = time.perf_counter()
+        r = ph_dist.run(n, 200, crops=1, rho=1.0, convthresh=1e-4, limit=limit)
+        wall = time.perf_counter() - t0
+        out["runs"].append({"ranks": n, "solves": r["subproblem_solves"],
+                            "seconds": round(r["seconds_to_tol"], 3),
+                            "solves_per_s": round(r["subproblem_solves"] / r["seconds_to_tol"], 1),
+                            "iterations": r["iterations"], "wall_with_startup": round(wall, 1)})
+        print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":  # (spawned ranks re-import this module)
+    main()
