@@ -26,6 +26,8 @@
 #include <vector>
 
 #include "../../include/phgpu.h"
+#include <atomic>
+
 #include "kkt_symbolic.h"
 #include "kkt_super.h"
 
@@ -4127,6 +4129,7 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
     return fail(PH_EHIP, "ph_batch_create: copying the pattern failed");
   }
   *out = b;
+  g_live_batches.fetch_add(1);
   return PH_OK;
 }
 
@@ -4316,17 +4319,24 @@ static int phase_event(ph_batch *b, int kind) {
 }
 
 // Kernels whose blocks wait for each other (the persistent loop's grid
-// barrier, the big path's team barriers) go through a cooperative launch:
-// the runtime either places every block of the grid at once or refuses the
-// launch, instead of a plain launch that can leave blocks waiting for CUs
-// held by another stream's (a spoke's) spinning kernel until the barrier's
-// tick budget aborts.  A stream being captured into a graph takes the plain
-// launch (graphs are opt-in and single-cylinder);
-// PHGPU_COOP=0: plain launches (measurement hook).  *placed = false: the
-// cooperative launch was refused as too large (the caller falls back).
+// barrier, the big path's team barriers) go through a cooperative launch
+// when another batch lives in the process (a hub's spokes, each with a
+// stream of its own): the runtime either places every block of the grid at
+// once or refuses the launch, instead of a plain launch that can leave
+// blocks waiting for CUs held by another stream's spinning kernel until the
+// barrier's tick budget aborts.  With one batch its kernels are ordered on
+// one stream and the plain launch is used (the cooperative one measured
+// 25 ms slower over F2's PH to 1e-4: 0.268 against 0.244 s,
+// profiles/r05/coop_ab.txt).  A stream being captured into a graph takes
+// the plain launch (graphs are opt-in and single-cylinder).
+// PHGPU_COOP=1 / 0 forces cooperative / plain launches.  *placed = false:
+// the cooperative launch was refused as too large (the caller fails).
+static std::atomic<int> g_live_batches{0};
+
 static bool coop_enabled() {
   const char *e = std::getenv("PHGPU_COOP");
-  return !(e && *e && std::atoi(e) == 0);
+  if (e && *e) return std::atoi(e) != 0;
+  return g_live_batches.load() > 1;
 }
 
 static int launch_coop(const void *f, dim3 grid, dim3 block, void **args, size_t lds, hipStream_t s,
@@ -5424,6 +5434,7 @@ void ph_batch_destroy(ph_batch_t b) {
   for (hipEvent_t e : b->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : b->pev) (void)hipEventDestroy(e);
   delete b;
+  g_live_batches.fetch_sub(1);
 }
 
 }  // extern "C"
