@@ -36,6 +36,7 @@
 namespace {
 
 thread_local std::string g_err;
+std::atomic<int> g_live_batches{0};  // batches alive in the process (coop_enabled)
 
 int fail(int code, const std::string &msg) {
   g_err = msg;
@@ -2572,6 +2573,11 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
 // one-wave PDHG solve (its warm polish first), then -- short of the
 // tolerance -- the LDL' rescue polish and the safe bound (miss_tail).  One
 // launch for what were pdhg_kernel, the rescue kernel and bound_kernel.
+// (its list is usually empty and it is launched every pass: its entry
+// reads the list count straight from the kernel arguments -- miss_tail is
+// inlined, so no per-lane scratch copy of SolveArgs / MidArgs is made; that
+// copy wrote ~3.9 MB of scratch per launch, 5.2 us of F2's 60 us pass,
+// profiles/r04/pmc_summary_f2.json)
 template <int E>
 __global__ void __launch_bounds__(WAVE) tail_kernel(SolveArgs a, MidArgs md, int has_md) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -2579,7 +2585,7 @@ __global__ void __launch_bounds__(WAVE) tail_kernel(SolveArgs a, MidArgs md, int
   if (count <= (int)blockIdx.x || (has_md && !ws_block_ok(md, a.err))) return;
   for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {  // uniform over the block
     const int s = list_entry(a.wl2, idx, a.S, a.err);
-    if (s >= 0) miss_tail<E>(a, has_md ? &md : nullptr, s, lds);
+    if (s >= 0) miss_tail<E>(a, md, has_md, s, lds);
   }
 }
 
@@ -4331,8 +4337,6 @@ static int phase_event(ph_batch *b, int kind) {
 // the plain launch (graphs are opt-in and single-cylinder).
 // PHGPU_COOP=1 / 0 forces cooperative / plain launches.  *placed = false:
 // the cooperative launch was refused as too large (the caller fails).
-static std::atomic<int> g_live_batches{0};
-
 static bool coop_enabled() {
   const char *e = std::getenv("PHGPU_COOP");
   if (e && *e) return std::atoi(e) != 0;
@@ -4393,7 +4397,7 @@ static int big_init(ph_batch *b) {
   }
   HIP_OK(hipFuncSetAttribute((const void *)big_polish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)b->big_plds_bytes));
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, big_polish_kernel, BIG_BLOCK,
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, big_polish_kernel, BIG_PBLOCK,
                                                       b->big_plds_bytes));
   if (per_cu < 1 || per_cu_p < 1) return fail(PH_EINVAL, "ph_batch_bind: the big-path kernels cannot be resident");
   int grid = std::min(b->S, std::min(per_cu, per_cu_p) * std::max(1, cus));
@@ -4589,7 +4593,7 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode, 0, 0};
     if (int rc = phase_event(b, 1)) return rc;
     if (b->big) {
-      hipLaunchKernelGGL(big_polish_kernel, dim3(b->big_grid), dim3(BIG_BLOCK), b->big_plds_bytes, b->stream,
+      hipLaunchKernelGGL(big_polish_kernel, dim3(b->big_grid), dim3(BIG_PBLOCK), b->big_plds_bytes, b->stream,
                          a, b->md, b->bg, ph);
       HIP_OK(hipGetLastError());
       return phase_event(b, -1);

@@ -43,8 +43,17 @@ def report(tag):
 lib.ph_debug_prof(b.handle, 1, None)
 ph.Iter0()
 report("Iter0")
+import time  # noqa: E402
+import torch  # noqa: E402
+b.set_timing(True)
 for k in range(NIT):
     lib.ph_debug_prof(b.handle, 1, None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     ph.Compute_Xbar(); ph.Update_W(False)
     ph.solve_loop(solver_options=ph.current_solver_options)
-    report(f"PH iteration {k + 1}")
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    it = b.iters.cpu().numpy()
+    report(f"PH iteration {k + 1} ({dt * 1000:.1f} ms; PDHG steps max {it.max()}, scenarios with steps "
+           f"{int((it > 0).sum())})")
