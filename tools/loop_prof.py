@@ -37,16 +37,20 @@ for mode in ("1", "0", "1"):
     os.environ["PHGPU_PERSIST"] = mode
     out = np.zeros(32, dtype=np.int64)
     lib.ph_debug_prof(b.handle, 1, None)
+    b.set_timing(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ph.run_device_loop(it, it + NIT, -1.0, chunk=NIT)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / NIT * 1e6
+    lk = b.loop_read_timing()
+    b.set_timing(False)
     lib.ph_debug_prof(b.handle, 0, out.ctypes.data_as(ctypes.c_void_p))
     it += NIT
     st = b.loop_status()
     print(f"PHGPU_PERSIST={mode}: passes {it - NIT}..{it}: {dt:.1f} us per pass (wall), "
-          f"misses {(st[3] - st[7]) / NIT:.1f} per pass", flush=True)
+          f"misses {(st[3] - st[7]) / NIT:.1f} per pass, PDHG solves {st[3] - st[6] - st[7]}; "
+          f"loop_kernel launches {lk[0]:.0f} ({lk[1] * 1e3 / NIT:.1f} us per pass inside them)", flush=True)
     if mode == "1":
         P = max(out[25], 1)
         nb = (S + 3) // 4 if S < 1024 else 256
@@ -56,3 +60,5 @@ for mode in ("1", "0", "1"):
               f"barrier-S {us(out[24]):.2f} us; slowest block's S {out[26] / 100.0 / P:.2f} us; "
               f"polishes {out[28]} ({out[28] / P:.1f}/pass) at {out[27] / 100.0 / max(out[28], 1):.2f} us each",
               flush=True)
+        print(f"  miss queue: {out[29] / P:.1f} queued/pass; drain {out[30] / 100.0 / P / (nb * 4):.2f} us per wave-pass; "
+              f"slowest polish {out[31] / 100.0:.2f} us", flush=True)
