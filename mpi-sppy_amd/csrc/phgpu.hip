@@ -2469,7 +2469,8 @@ __device__ __forceinline__ bool polish_one(const SolveArgs &a, int s, int lane, 
         XN_out = xn;
         return true;
       }
-      if (lane < n) a.x[(size_t)lane * S + s] = xn * DC;
+      // (x write-through: finish_kernel's later blocks read it in the launch)
+      if (lane < n) pub(a.x + (size_t)lane * S + s, xn * DC);
       if (lane < m) a.y[(size_t)lane * S + s] = yn * DR;
       if (lane == 0) {
         a.status[s] = PH_STATUS_OPTIMAL;
@@ -2513,12 +2514,15 @@ __device__ __forceinline__ void ph_lane_terms(const SolveArgs &a, int lane, doub
   }
 }
 
-__global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+// The misses of the cached solve's list wl, grid-strided over `nb` one-wave
+// blocks: the register polish from the hint; what it cannot finish goes to
+// the tail list wl2.
+__device__ __forceinline__ bool polish_pass(const SolveArgs &a, double *lds, int nb) {
   const int lane = threadIdx.x;
   const int S = a.S, n = a.n, m = a.m, nnz = a.nnz, K = a.K;
-  const int count = stopped(a.ctl) ? 0 : list_count(a.wl_count, a.S, a.err);
-  if ((int)blockIdx.x >= count) return;
+  const int count = list_count(a.wl_count, a.S, a.err);
+  if ((int)blockIdx.x >= count) return false;
+  bool pushed = false;  // (uniform: one wave)
   // LDS: staging rows | solutions | vals | xs | ys | pattern + maps
   double *kst = lds;                        // [RG_KST]: staging rows / product vectors
   double *sol = kst + RG_KST;               // [1+RG_K][WAVE]
@@ -2542,7 +2546,7 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
   const PolScratch ws{kst, sol, xs, ys, cpos, rpos};
   const PatLds pt{rp, ci, cp, cr, ck};
   const int kslot = lane < n ? a.slot_of_col[lane] : -1;
-  for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
+  for (int idx = blockIdx.x; idx < count; idx += nb) {
     const int s = list_entry(a.wl, idx, S, a.err);
     if (s < 0) continue;  // (uniform: one wave)
     __syncthreads();  // LDS of the previous scenario
@@ -2561,11 +2565,21 @@ __global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
     double XN = 0.0;
     const bool solved = polish_one(a, s, lane, ws, pt, vl, a.sb + (size_t)s * (4 * n + 3 * m), hk_l,
                                    qk_l, cst_l, kslot, sig0, nullptr, XN);
-    if (!solved && lane == 0) {  // tail_kernel: warm polish from the point, PDHG, rescue
-      a.hint_ok[s] = 0;
-      list_push(a.wl2, a.wl2_count, s, S, a.err);
+    if (!solved) {  // tail_kernel: warm polish from the point, PDHG, rescue
+      pushed = true;
+      if (lane == 0) {
+        a.hint_ok[s] = 0;
+        list_push(a.wl2, a.wl2_count, s, S, a.err);
+      }
     }
   }
+  return pushed;
+}
+
+__global__ void __launch_bounds__(WAVE) polish_kernel(SolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  if (stopped(a.ctl)) return;
+  polish_pass(a, lds, (int)gridDim.x);
 }
 
 // The misses the register polish could not finish (wl2), grid-strided over
@@ -2859,6 +2873,340 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
     }
   }
   if (gridDim.x > 1 && xa.C > 0) summary_last(xa, ctl);
+}
+
+// ------------------------------------------------------------------------
+// The end of a single-rank device-loop pass in ONE launch (finish_kernel):
+// what were polish_kernel, tail_kernel, summary_kernel and the next pass's
+// update_w_conv_kernel, four launches of ~4.5 us each at F2 whatever their
+// work (profiles/r05/f2_trace_window.txt).  One-wave blocks in four roles,
+// each later role waiting on a counter of the earlier one (a waiting block
+// only holds its slot; the blocks it waits for never wait on it):
+//   [0, np)          the register polish of the miss list (polish_pass);
+//                    blocks [0, tb) then wait for every polish block and run
+//                    the tail list wl2 (miss_tail: PDHG, rescue, bound)
+//   [np, np + nsum)  Compute_Xbar's sums of the pass's x in 256-scenario
+//                    chunks; the last one combines them in chunk order, the
+//                    solve's counters (summary_kernel's block 0) and the
+//                    iteration advance (loop_advance)
+//   [.., + nu)       the next pass's Compute_Xbar broadcast + Update_W +
+//                    convergence_diff (update_w_conv_kernel) over 256
+//                    scenarios each; the last one: conv in block order, the
+//                    stop test, the next solve's list counters (nu = 0: the
+//                    next pass starts with update_w_conv_kernel)
+// Data written in the launch and read by another block moves through
+// agent-scope atomics (pub / sub) or behind a release fence (a polish or
+// tail block's outputs; its done count after it).
+// ------------------------------------------------------------------------
+constexpr int FIN_CHUNK = 256;  // scenarios per sum / update block
+constexpr int FIN_DONE = 0, FIN_TAIL = 128, FIN_SUMT = 144, FIN_READY = 160, FIN_UT = 176, FIN_WORDS = 192;
+
+struct FinArgs {
+  XbarArgs xa;          // the pass's Compute_Xbar sums (xa.out) over its slot ranges; xa.part unused
+  int np, tb, nsum, nu, C;  // role sizes; C chunks per slot
+  int32_t *fin;         // [FIN_WORDS] counters (zero between launches)
+  double *part;         // [nsum][2] sum partials, then [nu] conv partials
+  unsigned long long *summary;  // the solve's counters (summary_kernel's out)
+  // update_w_conv of the next pass
+  const int32_t *gid;
+  const double *rho, *wc, *wconv;
+  double *xbar, *xsqbar, *W, *absdiff, *hist;
+  int has_md;
+  unsigned long long *prof;  // phase stamps (ph_debug_prof slots 16-19, 29-31) or null
+};
+
+__device__ __forceinline__ int fin_load(const int32_t *p) {
+  return __hip_atomic_load(const_cast<int32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fin_wait(const int32_t *p, int target, int shards, int32_t *err) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      int v = 0;
+      for (int g = 0; g < shards; ++g) v += fin_load(p + 16 * g);
+      if (v >= target) break;
+      if (wall_clock64() - t0 > 400000000ull) {  // 4 s (never expected: every producer is running)
+        dev_fail(err, CHK_BARRIER, target, v);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ int fin_ticket(int32_t *p) {  // (thread 0) after the block's publishing stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// n published doubles into LDS by one wave, four loads in flight per lane
+// (a lane-serial loop of atomic loads pays a round trip per value).
+__device__ __forceinline__ void fin_stage(double *dst, const double *src, int n, int lane) {
+  for (int q0 = 0; q0 < n; q0 += 4 * WAVE) {
+    double t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = q0 + u * WAVE + lane;
+      t[u] = q < n ? sub(src + q) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = q0 + u * WAVE + lane;
+      if (q < n) dst[q] = t[u];
+    }
+  }
+  wsync();
+}
+
+template <int E>
+__global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, FinArgs f) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  if (stopped(a.ctl)) return;  // (uniform: the flag changes only in the last sum / update block below)
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int S = a.S, K = a.K, G = f.xa.G;
+  int32_t *fin = f.fin;
+  LoopCtl *ctl = const_cast<LoopCtl *>(a.ctl);
+  // phase stamps (debug, the launch's): 16 block 0's start, 17 polish blocks'
+  // end, 18 tail blocks' end, 19 sums ready, 29 updates' end, 30 working
+  // polish blocks, 31 their longest release fence
+  if (f.prof && lane == 0 && b == 0) atomicExch(&f.prof[16], wall_clock64());
+  if (b < f.np) {
+    // ---- polish, then (blocks < tb) the tail list
+    // (the solutions' x went out write-through; a block that pushed a tail
+    // entry writes back what the tail blocks read: the entry, hint_ok)
+    if (polish_pass(a, lds, f.np)) {
+      const unsigned long long tf = f.prof ? wall_clock64() : 0ull;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (f.prof && lane == 0) {
+        atomicAdd(&f.prof[30], 1ull);
+        atomicMax(&f.prof[31], wall_clock64() - tf);
+      }
+    }
+    if (lane == 0) fin_ticket(fin + FIN_DONE + 16 * (b & 7));
+    if (f.prof && lane == 0) atomicMax(&f.prof[17], wall_clock64());
+    if (b >= f.tb) return;
+    fin_wait(fin + FIN_DONE, f.np, 8, a.err);
+    const int count = min(fin_load(a.wl2_count), S);
+    if (count == 0) return;  // (the usual case: the later blocks see the empty list too)
+    if (count > b && (!f.has_md || ws_block_ok(md, a.err))) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (int idx = b; idx < count; idx += f.tb) {
+        const int s = fin_load(a.wl2 + idx);
+        if (s < 0 || s >= S) {
+          if (lane == 0) dev_fail(a.err, CHK_ENTRY_RANGE, s, idx);
+          continue;
+        }
+        miss_tail<E>(a, md, f.has_md, s, lds);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+    if (lane == 0) fin_ticket(fin + FIN_TAIL);
+    if (f.prof && lane == 0) atomicMax(&f.prof[18], wall_clock64());
+    return;
+  }
+  if (b < f.np + f.nsum) {
+    // ---- Compute_Xbar: chunk j of slot g
+    const int j = b - f.np, g = j / f.C, c = j % f.C;
+    const XbarArgs &xa = f.xa;
+    const int k = xa.slot_k[g];
+    const double *xr = xa.x + (size_t)xa.nonant_col[k] * S;
+    const double *pr = xa.pc + (size_t)k * S;
+    const int c0 = xa.s0[g] + c * FIN_CHUNK, c1 = min(xa.s1[g], c0 + FIN_CHUNK);
+    double v0 = 0.0, v1 = 0.0;
+    {
+      double xv[FIN_CHUNK / WAVE], p[FIN_CHUNK / WAVE];
+#pragma unroll
+      for (int u = 0; u < FIN_CHUNK / WAVE; ++u) {  // (static: before the wait)
+        const int s = c0 + u * WAVE + lane;
+        p[u] = s < c1 ? pr[s] : 0.0;
+      }
+      fin_wait(fin + FIN_DONE, f.np, 8, a.err);
+      if (fin_load(a.wl2_count) > 0) fin_wait(fin + FIN_TAIL, f.tb, 1, a.err);
+#pragma unroll
+      for (int u = 0; u < FIN_CHUNK / WAVE; ++u) {  // all loads in flight
+        const int s = c0 + u * WAVE + lane;
+        xv[u] = s < c1 ? sub(xr + s) : 0.0;  // (x: written in this launch)
+      }
+#pragma unroll
+      for (int u = 0; u < FIN_CHUNK / WAVE; ++u) {
+        v0 += p[u] * xv[u];
+        v1 += p[u] * xv[u] * xv[u];
+      }
+    }
+    v0 = wave_sum(v0);
+    v1 = wave_sum(v1);
+    if (lane == 0) {
+      pub(f.part + 2 * (size_t)j, v0);
+      pub(f.part + 2 * (size_t)j + 1, v1);
+    }
+    int last = 0;
+    if (lane == 0) last = fin_ticket(fin + FIN_SUMT) == f.nsum - 1;
+    if (!__shfl(last, 0, WAVE)) return;
+    // the last chunk: the sums in chunk order, the counters, the advance
+    fin_stage(lds, f.part, 2 * f.nsum, lane);
+    for (int gg = lane; gg < G; gg += WAVE) {
+      double a0 = 0.0, a1 = 0.0;
+      for (int cc = 0; cc < f.C; ++cc) {
+        a0 += lds[2 * ((size_t)gg * f.C + cc)];
+        a1 += lds[2 * ((size_t)gg * f.C + cc) + 1];
+      }
+      pub(xa.out + gg, a0);
+      pub(xa.out + G + gg, a1);
+    }
+    // summary_kernel's block 0 over the tail list: (not optimal, iters sum,
+    // iters max, polished, cached)
+    unsigned long long v[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
+    const int nl = min(fin_load(a.wl2_count), S);
+    for (int q = lane; q < nl; q += WAVE) {
+      const int s = fin_load(a.wl2 + q);
+      if (s < 0 || s >= S) {
+        dev_fail(a.err, CHK_ENTRY_RANGE, s, q);
+        continue;
+      }
+      const int st = fin_load(a.status + s);
+      const unsigned long long it = (unsigned long long)fin_load(a.iters + s);
+      const double hw = sub(a.diag + PH_DIAG_W * (size_t)s + 4);
+      v[0] += st != PH_STATUS_OPTIMAL;
+      v[1] += it;
+      v[2] = it > v[2] ? it : v[2];
+      v[3] += hw == 1.0 || hw == 2.0;
+      v[4] += hw == 3.0;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const unsigned long long o = __shfl_xor(v[i], off, WAVE);
+        v[i] = i == 2 ? (o > v[i] ? o : v[i]) : v[i] + o;
+      }
+    if (lane == 0) {
+      const int c0l = list_count(a.wl_count, S, a.err);
+      v[3] += (unsigned long long)max(c0l - nl, 0);
+      v[4] += (unsigned long long)(S - c0l);
+      for (int i = 0; i < 5; ++i) f.summary[i] = v[i];
+      ctl->acc[0] += v[0];
+      ctl->acc[1] += (unsigned long long)S;
+      ctl->acc[2] += v[1];
+      ctl->acc[3] = v[2] > ctl->acc[3] ? v[2] : ctl->acc[3];
+      ctl->acc[4] += v[3];
+      ctl->acc[5] += v[4];
+      // loop_advance, stores the update blocks read through atomics
+      const int stp = ctl->stop, itn = ctl->iter;
+      if (!stp) {
+        if (itn >= ctl->limit) __hip_atomic_store(&ctl->stop, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_store(&ctl->iter, itn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (f.prof) atomicMax(&f.prof[19], wall_clock64());
+      if (f.nu > 0) {
+        fin_ticket(fin + FIN_READY);  // (after the sums' and the control's stores)
+      } else {  // the launch's counters back to zero
+        for (int q = 0; q < 8; ++q) __hip_atomic_store(fin + FIN_DONE + 16 * q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fin + FIN_TAIL, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fin + FIN_SUMT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
+  // ---- the next pass's Compute_Xbar broadcast + Update_W + convergence_diff
+  // (lanes over (slot, scenario) pairs of the block's scenarios; the sums
+  // staged in LDS; per-scenario |d| sums in slot order)
+  const int u = b - f.np - f.nsum;
+  double *sl = lds, *adv = lds + 2 * G;  // [2G] sums, [K][FIN_CHUNK] |d|
+  const int sb0 = u * FIN_CHUNK, nsb = min(FIN_CHUNK, S - sb0);
+  const int npair = K * FIN_CHUNK;
+  constexpr int PV = 4 * FIN_CHUNK / WAVE;  // pairs per lane per round (one round for K <= 4)
+  constexpr int SV = FIN_CHUNK / WAVE;      // scenarios per lane
+  double wcv[SV];
+#pragma unroll
+  for (int v = 0; v < SV; ++v) {
+    const int j = v * WAVE + lane;
+    wcv[v] = j < nsb ? f.wconv[sb0 + j] : 0.0;
+  }
+  bool stop_now = false;
+  for (int e0 = 0; e0 < npair; e0 += PV * WAVE) {
+    int gg[PV];
+    double wv[PV], rv[PV], cv[PV], xv[PV];
+#pragma unroll
+    for (int v = 0; v < PV; ++v) {  // the static operands before the waits
+      const int e = e0 + v * WAVE + lane, k = e / FIN_CHUNK, j = e - k * FIN_CHUNK;
+      const bool in = e < npair && j < nsb;
+      const size_t o = (size_t)k * S + sb0 + j;
+      gg[v] = in ? f.gid[o] : 0;
+      wv[v] = in ? f.W[o] : 0.0;
+      rv[v] = in ? f.rho[o] : 0.0;
+      cv[v] = in && f.wc ? f.wc[o] : 1.0;
+    }
+    if (e0 == 0) {  // the pass's x once the polish and the tail are done
+      fin_wait(fin + FIN_DONE, f.np, 8, a.err);
+      if (fin_load(a.wl2_count) > 0) fin_wait(fin + FIN_TAIL, f.tb, 1, a.err);
+    }
+#pragma unroll
+    for (int v = 0; v < PV; ++v) {
+      const int e = e0 + v * WAVE + lane, k = e / FIN_CHUNK, j = e - k * FIN_CHUNK;
+      xv[v] = e < npair && j < nsb ? sub(a.x + (size_t)a.nonant_col[k] * S + sb0 + j) : 0.0;
+    }
+    if (e0 == 0) {  // then the sums
+      fin_wait(fin + FIN_READY, 1, 1, a.err);
+      stop_now = fin_load(&ctl->stop) != 0;  // (the iteration limit, set above)
+      if (!stop_now) fin_stage(sl, f.xa.out, 2 * G, lane);
+    }
+    if (stop_now) break;
+#pragma unroll
+    for (int v = 0; v < PV; ++v) {
+      const int e = e0 + v * WAVE + lane, k = e / FIN_CHUNK, j = e - k * FIN_CHUNK;
+      if (e >= npair || j >= nsb) continue;
+      const size_t o = (size_t)k * S + sb0 + j;
+      const double xb = sl[gg[v]], xsq = sl[G + gg[v]];
+      f.xbar[o] = xb;
+      f.xsqbar[o] = xsq;
+      const double d = xv[v] - xb;
+      double w = wv[v] + rv[v] * d;
+      if (f.wc) w *= cv[v];
+      f.W[o] = w;
+      adv[e] = fabs(d);
+    }
+  }
+  double cw = 0.0;
+  if (!stop_now) {
+    wsync();
+#pragma unroll
+    for (int v = 0; v < SV; ++v) {
+      const int j = v * WAVE + lane;
+      if (j >= nsb) continue;
+      double acc = 0.0;
+      for (int k = 0; k < K; ++k) acc += adv[(size_t)k * FIN_CHUNK + j];
+      f.absdiff[sb0 + j] = acc;
+      cw += acc * wcv[v];
+    }
+  }
+  cw = wave_sum(cw);
+  double *pc = f.part + 2 * (size_t)f.nsum;
+  if (lane == 0) pub(pc + u, cw);
+  int last = 0;
+  if (lane == 0) last = fin_ticket(fin + FIN_UT) == f.nu - 1;
+  if (!__shfl(last, 0, WAVE)) return;
+  if (!stop_now) fin_stage(lds, pc, f.nu, lane);
+  if (lane == 0) {
+    if (!stop_now) {
+      double conv = 0.0;
+      for (int q = 0; q < f.nu; ++q) conv += lds[q];
+      const int itn = fin_load(&ctl->iter);
+      f.hist[itn - 1] = conv;
+      if (conv < ctl->thresh) ctl->stop = 1;
+    }
+    // the next solve's list counters (update_w_conv_kernel's), this launch's
+    int32_t *ctr = a.wl_count;  // (== the batch's ctr: wl_count, queue, wl2_count at 0, 1, 2; ul at 6)
+    ctr[0] = 0;
+    ctr[1] = 0;
+    ctr[2] = 0;
+    ctr[6] = 0;
+    for (int q = 0; q < 8; ++q) __hip_atomic_store(fin + FIN_DONE + 16 * q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(fin + FIN_TAIL, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(fin + FIN_SUMT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(fin + FIN_READY, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(fin + FIN_UT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f.prof) atomicMax(&f.prof[29], wall_clock64());
+  }
 }
 
 // Single-rank device loop: Compute_Xbar's broadcast + Update_W (as
@@ -3465,6 +3813,11 @@ struct ph_batch {
   double *d_c = nullptr, *d_l = nullptr, *d_u = nullptr, *d_rl = nullptr, *d_ru = nullptr;
   double *d_diag = nullptr;
   unsigned long long *d_summary = nullptr;
+  int32_t *d_fin = nullptr;     // [FIN_WORDS] finish_kernel's counters
+  double *d_fpart = nullptr;    // finish_kernel's partials
+  size_t fpart_cap = 0;
+  bool fin_attr = false;
+  bool primed = false;          // the first cached solve's hints were seeded (prime_hints)
   // active-set cache (polish-size scenarios): [S][CW] doubles + flags
   int CW = 0;
   double *d_cache = nullptr;
@@ -4671,6 +5024,66 @@ __global__ void __launch_bounds__(256) gather_kernel(const double *__restrict__ 
 // The one-wave path without the active-set cache (Iter0, cold or bound
 // solves): pdhg_kernel over every scenario, then the rescue polish of the
 // ones it left at the iteration limit (its list) and their safe bounds.
+// The first cached solve of a batch (Iter0) has no cache entries and no
+// hints: every scenario would start its register polish from an empty
+// active set and most would fall to the cold PDHG.  Scenarios of one model
+// mostly share their optimal active set, so R representatives (s = q S / R)
+// are solved first (pdhg_kernel on their list) and each scenario's hint is
+// seeded with its representative's active set (classify_trial on the
+// representative's scaled solution); the cached path then polishes every
+// scenario from it, and only what the polish cannot finish goes to PDHG.
+constexpr int PRIME_REPS = 8;
+constexpr double PRIME_TOL = 1e-3, PRIME_TH = 1e-3;
+__global__ void __launch_bounds__(WAVE) prime_list_kernel(int32_t *wl, int32_t *count, int S, int R) {
+  for (int q = threadIdx.x; q < R; q += WAVE) wl[q] = (int)((long)q * S / R);
+  if (threadIdx.x == 0) count[0] = R;
+}
+__global__ void __launch_bounds__(WAVE) prime_hint_kernel(SolveArgs a, int R) {
+  const int lane = threadIdx.x, S = a.S, n = a.n, m = a.m;
+  const int s0 = blockIdx.x * WAVE;
+  if (s0 >= S) return;
+  const int r = (int)((long)s0 * R / S), sr = (int)((long)r * S / R);  // the wave's representative
+  const double *sb = a.sb + (size_t)sr * (4 * n + 3 * m);
+  double x = 0.0, y = 0.0, L = 0.0, U = 0.0, RL = 0.0, RU = 0.0;
+  if (lane < n) {
+    L = sb[n + lane];
+    U = sb[2 * n + lane];
+    x = a.x[(size_t)lane * S + sr] / sb[3 * n + lane];
+  }
+  if (lane < m) {
+    RL = sb[4 * n + lane];
+    RU = sb[4 * n + m + lane];
+    y = a.y[(size_t)lane * S + sr] / sb[4 * n + 2 * m + lane];
+  }
+  const ActiveSet as = classify_trial(lane, n, m, PRIME_TH, x, y, L, U, RL, RU);
+  unsigned long long sig[4];
+  as.signature(sig);
+  const int s = s0 + lane;
+  if (s < S) {
+    for (int i = 0; i < 4; ++i) a.hint[4 * (size_t)s + i] = sig[i];
+    a.hint_ok[s] = 1;
+  }
+}
+
+static int prime_hints(ph_batch *b, SolveArgs a, size_t lds) {
+  const int R = std::min(b->S, PRIME_REPS);
+  hipLaunchKernelGGL(prime_list_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_wl, b->d_ctr, b->S, R);
+  HIP_OK(hipMemsetAsync(b->d_ctr + 1, 0, sizeof(int32_t), b->stream));  // (pdhg_kernel's queue)
+  a.wl = b->d_wl;
+  a.ul = nullptr;  // (a representative short of the tolerance still seeds a hint)
+  // a hint needs the active set, not the tolerance: PDHG to 1e-3 (the
+  // representatives are polished again with everyone else)
+  a.tol = std::max(a.tol, PRIME_TOL);
+  a.polish = 0;
+  DISPATCH_EXT(64, 1, b->ext, {
+    hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(R), dim3(B_), lds, b->stream, a);
+  });
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(prime_hint_kernel, dim3((b->S + WAVE - 1) / WAVE), dim3(WAVE), 0, b->stream, a, R);
+  HIP_OK(hipGetLastError());
+  return PH_OK;
+}
+
 static int cold_tail(ph_batch *b, SolveArgs &a, size_t lds) {
   DISPATCH_EXT(64, 1, b->ext, {
     hipLaunchKernelGGL((pdhg_kernel<B_, P_, E_>), dim3(std::min(b->S, b->pdhg_grid)), dim3(B_), lds,
@@ -4764,7 +5177,7 @@ static int ensure_pdhg_grid(ph_batch *b, size_t lds) {
 
 // tail_kernel over the tail list wl2 (the cached solve's misses the register
 // polish left): a small grid, its blocks exit at once when the list is empty.
-static int launch_tail(ph_batch *b, const SolveArgs &a, size_t lds) {
+static int launch_tail(ph_batch *b, const SolveArgs &a, size_t lds, int grid_cap = 0) {
   const int has_md = one_wave_rescue(b) ? 1 : 0;
   if (has_md)
     if (int rc = mid_init(b)) return rc;
@@ -4780,7 +5193,8 @@ static int launch_tail(ph_batch *b, const SolveArgs &a, size_t lds) {
       const char *e = std::getenv("PHGPU_TAIL_GRID");
       return e ? std::min(TAIL_GRID, std::max(1, std::atoi(e))) : 64;
     }();
-    hipLaunchKernelGGL((tail_kernel<E_>), dim3(std::min(b->S, std::min(b->pdhg_grid, tail_grid))),
+    const int tg = grid_cap > 0 ? std::max(tail_grid, grid_cap) : tail_grid;
+    hipLaunchKernelGGL((tail_kernel<E_>), dim3(std::min(b->S, std::min(b->pdhg_grid, tg))),
                        dim3(WAVE), tlds, b->stream, a, b->md, has_md);
   });
   HIP_OK(hipGetLastError());
@@ -4804,6 +5218,18 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
   if (int rc = ensure_pdhg_grid(b, lds)) return rc;
+  static const int prime_env = [] {  // PHGPU_PRIME=0: off (A/B hook)
+    const char *e = std::getenv("PHGPU_PRIME");
+    return e && *e ? std::atoi(e) : 1;
+  }();
+  if (prime_env && a.cache && a.warm && !b->primed && !b->loop_on && b->S > PRIME_REPS) {
+    // (hints of the first cached solve; needs the hint arrays in a)
+    SolveArgs ap = a;
+    ap.hint = b->d_hint;
+    ap.hint_ok = b->d_hint_ok;
+    if (int rc = prime_hints(b, ap, lds)) return rc;
+    b->primed = true;
+  }
   // (in the device loop the convergence kernel has cleared the counters)
   if (!b->loop_on) {
     HIP_OK(hipMemsetAsync(b->d_ctr, 0, 3 * sizeof(int32_t), b->stream));
@@ -4863,7 +5289,9 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     HIP_OK(hipGetLastError());
     if (tev) HIP_OK(hipEventRecord(tev[2], b->stream));  // (polish | tail: separate times)
     a.ul = nullptr;  // (the tail bounds its failures itself)
-    if (int rc = launch_tail(b, a, lds)) return rc;
+    // (outside the device loop -- Iter0, bounds, xhat -- the tail list can
+    // be long: a wider grid; in the loop it is short and the launch small)
+    if (int rc = launch_tail(b, a, lds, b->loop_on ? 0 : TAIL_GRID)) return rc;
     if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
   } else {
     if (tev) {
@@ -5237,6 +5665,129 @@ int ph_loop_read_timing(ph_batch_t b, double *out) {
   return PH_OK;
 }
 
+// The fused single-rank pass (finish_kernel) applies: one rank, the
+// one-wave cached warm solve, the device loop's Compute_Xbar sums bound to
+// this pass, not under stream capture (a captured chunk replays its first
+// pass's update_w_conv), the tail's LDS small (PHGPU_FUSED=0: off, A/B hook).
+static bool fused_ok(ph_batch *b, size_t *fin_lds, int *has_md) {
+  static const int env = [] {
+    const char *e = std::getenv("PHGPU_FUSED");
+    return e && *e ? std::atoi(e) : 1;
+  }();
+  const ph_loop_pass_args &p = b->pass;
+  if (!env || p.conv_part || b->mid || !polish_fits(b) || !b->d_sb || !b->d_cache || !p.opts.polish ||
+      !p.opts.warm_start || b->K <= 0 || p.G <= 0 || b->loop_xa.G != p.G || b->loop_xa.C <= 0 ||
+      b->loop_xa.x != p.x || b->loop_xa.out != p.sums)
+    return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(b->stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  *has_md = one_wave_rescue(b) ? 1 : 0;
+  size_t t = solve_lds_bytes(b);
+  if (*has_md) t = std::max(t, b->mid_plds_bytes);
+  t = std::max(t, polish_lds_bytes(b));
+  {  // the sum / update blocks' staging
+    const size_t C = (b->S + FIN_CHUNK - 1) / FIN_CHUNK;
+    t = std::max(t, sizeof(double) * std::max(2 * (size_t)p.G * C, 2 * (size_t)p.G + (size_t)b->K * FIN_CHUNK));
+  }
+  if (t > 64 * 1024) return false;  // (a big tail carve would cost the polish blocks' occupancy)
+  *fin_lds = t;
+  return true;
+}
+
+// One fused pass: [update_w_conv when `first`] -> active_set_kernel ->
+// finish_kernel (polish, tail, Compute_Xbar sums + counters + advance, and
+// when `u_next` the next pass's update_w_conv).
+static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds, int has_md) {
+  const ph_loop_pass_args &p = b->pass;
+  if (first)
+    if (int rc = launch_update_w_conv(b, p.x, p.sums, p.G, p.gid, p.rho, p.w_coeff, p.xbar, p.xsqbar, p.W,
+                                      p.absdiff, p.wconv, p.conv_hist, nullptr))
+      return rc;
+  SolveArgs a;
+  fill_solve_args(b, p.W, p.rho, p.xbar, p.w_on, p.prox_on, p.x, p.y, p.omega, p.status, p.iters, p.pobj,
+                  p.dbound, &p.opts, a);
+  if (!(a.tol > 0.0) || a.max_iters <= 0) return fail(PH_EINVAL, "ph_loop_run: bad options");
+  const size_t lds = solve_lds_bytes(b);
+  if (int rc = ensure_pdhg_grid(b, lds)) return rc;
+  if (has_md)
+    if (int rc = mid_init(b)) return rc;
+  a.hint = b->d_hint;
+  a.hint_ok = b->d_hint_ok;
+  a.wl = b->d_wl;
+  a.wl2 = b->d_wl2;
+  a.ul = nullptr;
+  hipEvent_t *tev = nullptr;
+  if (b->timing) {
+    if (b->ev_used + 4 > b->ev.size()) {
+      for (int i = 0; i < 4; ++i) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreate(&e));
+        b->ev.push_back(e);
+      }
+    }
+    tev = &b->ev[b->ev_used];
+    b->ev_used += 4;
+    HIP_OK(hipEventRecord(tev[0], b->stream));
+  }
+  {
+    constexpr int WPB = 4;
+    const size_t as_lds = sizeof(double) * WPB * ((size_t)b->CW + 4 * b->n + 3 * b->m + WAVE);
+    hipLaunchKernelGGL((active_set_kernel<WPB, 1>), dim3((b->S + WPB - 1) / WPB), dim3(WPB * WAVE), as_lds,
+                       b->stream, a);
+    HIP_OK(hipGetLastError());
+  }
+  if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
+  FinArgs f;
+  f.xa = b->loop_xa;
+  f.C = (b->S + FIN_CHUNK - 1) / FIN_CHUNK;
+  f.np = std::min(b->S, 1024);
+  f.tb = std::min(f.np, 64);
+  if (has_md && b->md.ws_g) f.tb = std::max(1, std::min(f.tb, b->md.ws_blocks));
+  f.nsum = p.G * f.C;
+  f.nu = u_next ? f.C : 0;
+  f.has_md = has_md;
+  const size_t need = 2 * (size_t)f.nsum + (size_t)f.C;
+  if (!b->d_fin) {
+    if (int rc = dalloc(&b->d_fin, FIN_WORDS)) return rc;
+    HIP_OK(hipMemsetAsync(b->d_fin, 0, FIN_WORDS * sizeof(int32_t), b->stream));
+  }
+  if (need > b->fpart_cap) {
+    if (b->d_fpart) HIP_OK(hipFree(b->d_fpart));
+    b->d_fpart = nullptr;
+    if (int rc = dalloc(&b->d_fpart, need)) return rc;
+    b->fpart_cap = need;
+  }
+  f.fin = b->d_fin;
+  f.part = b->d_fpart;
+  f.summary = b->d_summary;
+  f.gid = p.gid;
+  f.rho = p.rho;
+  f.wc = p.w_coeff;
+  f.wconv = p.wconv;
+  f.xbar = p.xbar;
+  f.xsqbar = p.xsqbar;
+  f.W = p.W;
+  f.absdiff = p.absdiff;
+  f.hist = p.conv_hist;
+  f.prof = a.prof;  // (ph_debug_prof on: stamps; the polish's own clocks off)
+  a.prof = nullptr;
+  DISPATCH_EXT(64, 1, b->ext, {
+    if (!b->fin_attr && fin_lds > 64 * 1024) {
+      HIP_OK(hipFuncSetAttribute((const void *)finish_kernel<E_>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)fin_lds));
+      b->fin_attr = true;
+    }
+    hipLaunchKernelGGL((finish_kernel<E_>), dim3(f.np + f.nsum + f.nu), dim3(WAVE), fin_lds, b->stream, a, b->md,
+                       f);
+  });
+  HIP_OK(hipGetLastError());
+  if (tev) {
+    HIP_OK(hipEventRecord(tev[2], b->stream));
+    HIP_OK(hipEventRecord(tev[3], b->stream));
+  }
+  return PH_OK;
+}
+
 int ph_loop_run(ph_batch_t b, int32_t iters) {
   if (!b || !b->loop_on || !b->pass_bound)
     return fail(PH_EINVAL, "ph_loop_run: loop not enabled or no pass bound");
@@ -5244,6 +5795,13 @@ int ph_loop_run(ph_batch_t b, int32_t iters) {
   bool persist = false;
   if (int rc = loop_persist_setup(b, &persist)) return rc;
   if (!persist) {  // the per-pass kernels
+    size_t fin_lds = 0;
+    int has_md = 0;
+    if (fused_ok(b, &fin_lds, &has_md)) {  // three launches per pass -> two
+      for (int i = 0; i < iters; ++i)
+        if (int rc = loop_pass_fused(b, i == 0, i + 1 < iters, fin_lds, has_md)) return rc;
+      return PH_OK;
+    }
     for (int i = 0; i < iters; ++i)
       if (int rc = ph_loop_pass(b)) return rc;
     return PH_OK;
@@ -5431,7 +5989,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
                   b->d_ctl, b->d_sym, b->d_sym16, b->d_ssym, b->d_ksdev, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
-                  b->d_bws, b->d_lpart, b->d_lbar, b->d_teambar, b->d_teampart,
+                  b->d_bws, b->d_lpart, b->d_lbar, b->d_fin, b->d_fpart, b->d_teambar, b->d_teampart,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

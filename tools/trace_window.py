@@ -18,7 +18,7 @@ def nm(r):
     return r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:40]
 
 
-idx = [i for i, r in enumerate(rows) if "update_w_conv" in nm(r)]
+idx = [i for i, r in enumerate(rows) if "active_set" in nm(r)]
 seq = rows[idx[p0]:idx[p0 + NP]]
 tot = (int(seq[-1]["End_Timestamp"]) - int(seq[0]["Start_Timestamp"])) / 1e3
 print(f"passes {p0 + 1}..{p0 + NP}: {tot:.1f} us, {tot / NP:.2f} us per pass")
