@@ -786,6 +786,7 @@ def run():
     ph.run_device_loop(args.warmup + args.steps, args.warmup + 2 * args.steps, -1.0,
                        chunk=args.steps)
     n_t, as_ms, po_ms, pd_ms, nk, k_ms, np_, p_ms = b.read_timing_full()
+    fused = b.loop_fused()  # (the timing window's passes took the fused form)
     lk_n, lk_ms, lk_passes = b.loop_read_timing()
     sb_ = b.loop_status()
     b.set_timing(False)
@@ -816,6 +817,15 @@ def run():
     pd_bytes = t_pdhg * solve_bytes_per_scenario(c) + t_iters * bytes_per_pdhg_iter(c)
     cand = [("active_set_kernel", as_ms, as_bytes), ("polish_kernel", po_ms, po_bytes),
             ("tail_kernel", pd_ms, pd_bytes)]
+    if fused:
+        # the fused pass (ph_loop_fused): the grouped cached-map kernel, then
+        # finish_kernel = polish + tail + Compute_Xbar sums (per scenario K
+        # x and probability reads) + the next pass's Update_W / convergence
+        # (per slot: gid, W, rho, x in; xbar, xsqbar, W out; per scenario
+        # absdiff out, its weight in)
+        upd_bytes = S_loc * (K * (4 + 8 * 6) + 16) + S_loc * K * 16
+        as_name = "active_set_g_kernel" if max(n, m) <= 32 else "active_set_kernel"
+        cand = [(as_name, as_ms, as_bytes), ("finish_kernel", po_ms + pd_ms, po_bytes + pd_bytes + upd_bytes)]
     if mid:
         # per launch: a phase kernel's share of the solve's data in + solution
         # out is not separable, so each phase is priced at the whole solve's

@@ -354,6 +354,11 @@ int ph_loop_pass(ph_batch_t b);
 int ph_loop_run(ph_batch_t b, int32_t iters);
 /* 1 when ph_loop_run takes the persistent path for the bound pass, else 0. */
 int ph_loop_persistent(ph_batch_t b);
+/* 1 when a ph_loop_run since the last ph_loop_reset ran the fused per-pass
+ * form (two launches per pass: the cached maps, then finish_kernel: polish,
+ * tail, Compute_Xbar sums and the next pass's Update_W / convergence
+ * test), else 0. */
+int ph_loop_fused(ph_batch_t b);
 /*
  * While timing is on (ph_batch_set_timing): the persistent launches' HIP
  * events, out[3] = {loop_kernel launches, their total ms, passes they ran

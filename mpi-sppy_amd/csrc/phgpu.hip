@@ -2025,6 +2025,89 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
   }  // scenarios of the wave
 }
 
+// The cached maps of 64 / LPS scenarios per wave (as_evalg: LPS lanes per
+// scenario when n, m <= LPS), four waves per block: F2 evaluates four
+// scenarios per wave in one pass of the chain active_set_kernel runs once
+// per scenario (bitwise the same checks).  Per wave in LDS: the scenarios'
+// entries, static blocks and values, the clipped case's scratch, the entry
+// flags.
+constexpr int ASG_WPB = 4;
+__host__ __device__ inline size_t asg_wave_doubles(int CW, int n, int m, int nnz, int LPS) {
+  const int NG = 64 / LPS;
+  return (size_t)NG * (CW + 4 * n + 3 * m + nnz) + WAVE + (NG + 1) / 2;
+}
+template <int LPS>
+__global__ void __launch_bounds__(ASG_WPB * WAVE) active_set_g_kernel(SolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  constexpr int NG = 64 / LPS;
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const int s0 = (blockIdx.x * ASG_WPB + w) * NG;
+  if (s0 >= a.S || stopped(a.ctl)) return;  // wave-uniform; no block barriers
+  const int S = a.S, n = a.n, m = a.m, K = a.K, CW = a.CW, nnz = a.nnz, SBW = 4 * n + 3 * m;
+  const int ns = min(NG, S - s0);
+  double *ENT = lds + (size_t)w * asg_wave_doubles(CW, n, m, nnz, LPS);
+  double *SBV = ENT + (size_t)NG * CW, *VLV = SBV + (size_t)NG * SBW, *xsw = VLV + (size_t)NG * nnz;
+  int32_t *OKV = (int32_t *)(xsw + WAVE);
+  // the PH terms of this lane's (scenario, slot) before the staging waits
+  const int gg = lane / LPS, gl = lane % LPS;
+  const int sh = s0 + (gg < ns ? gg : 0);
+  double W = 0.0, r = 0.0, xb = 0.0;
+  if (gl < K) {
+    W = a.W[(size_t)gl * S + sh];
+    r = a.rho[(size_t)gl * S + sh];
+    xb = a.xbar[(size_t)gl * S + sh];
+  }
+  const int ok = lane < ns ? a.cache_ok[s0 + lane] : 0;
+  wave_stage2(ENT, a.cache + (size_t)s0 * CW, ns * CW, SBV, a.sb + (size_t)s0 * SBW, ns * SBW, lane);
+  wave_stage2(VLV, a.vals_s + (size_t)s0 * nnz, ns * nnz, VLV, a.vals_s, 0, lane);
+  if (lane < NG) OKV[lane] = ok;
+  double hk2 = 0.0, qk2 = 0.0, cst2 = 0.0;  // (ph_lane_terms' values)
+  if (gl < K) {
+    hk2 = a.w_on * W - a.prox_on * r * xb;
+    qk2 = a.prox_on * r;
+    cst2 = a.prox_on * 0.5 * r * xb * xb;
+  }
+  wsync();
+  int jg[NG];
+#pragma unroll
+  for (int q = 0; q < NG; ++q) jg[q] = q < ns ? q : -1;
+  const int kslotg = gl < n ? a.slot_of_col[gl] : -1;
+  double XN2 = 0.0;
+  int rr[NG];
+  unsigned long long sg[NG][4];
+  as_evalg<LPS>(a, s0, jg, lane, ENT, SBV, VLV, OKV, a.P, xsw, hk2, qk2, cst2, kslotg, XN2, rr, sg, nullptr);
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {  // the misses: hint, list (active_set_kernel's)
+    if (q >= ns || rr[q] == AS_HIT) continue;
+    const int s = s0 + q;
+    if (rr[q] == AS_MOVED && lane < 4)
+      a.hint[4 * (size_t)s + lane] = lane == 0 ? sg[q][0] : lane == 1 ? sg[q][1] : lane == 2 ? sg[q][2] : sg[q][3];
+    if (lane == 0) {
+      a.hint_ok[s] = rr[q] == AS_MOVED ? 1 : 0;
+      list_push(a.wl, a.wl_count, s, S, a.err);
+    }
+  }
+}
+
+// active_set_g_kernel when the scenario fits 32 lanes (PHGPU_AS_GROUPED=0:
+// active_set_kernel, A/B hook); returns false when it does not apply.
+static bool launch_as_grouped(int n, int m, int CW, int nnz, int S, hipStream_t st, const SolveArgs &a) {
+  static const int env = [] {
+    const char *e = std::getenv("PHGPU_AS_GROUPED");
+    return e && *e ? std::atoi(e) : 1;
+  }();
+  if (!env || n > 32 || m > 32) return false;
+  const int LPS = (n <= 16 && m <= 16) ? 16 : 32, NG = 64 / LPS;
+  const size_t lds = sizeof(double) * ASG_WPB * asg_wave_doubles(CW, n, m, nnz, LPS);
+  if (lds > 64 * 1024) return false;
+  const int per_block = ASG_WPB * NG;
+  if (LPS == 16)
+    hipLaunchKernelGGL(active_set_g_kernel<16>, dim3((S + per_block - 1) / per_block), dim3(ASG_WPB * WAVE), lds, st, a);
+  else
+    hipLaunchKernelGGL(active_set_g_kernel<32>, dim3((S + per_block - 1) / per_block), dim3(ASG_WPB * WAVE), lds, st, a);
+  return true;
+}
+
 __global__ void __launch_bounds__(WAVE) zero_i32_kernel(int32_t *p, int n) {
   for (int i = threadIdx.x; i < n; i += WAVE) p[i] = 0;
 }
@@ -3818,6 +3901,7 @@ struct ph_batch {
   size_t fpart_cap = 0;
   bool fin_attr = false;
   bool primed = false;          // the first cached solve's hints were seeded (prime_hints)
+  bool fused_ran = false;       // a fused pass ran since ph_loop_reset (ph_loop_fused)
   // active-set cache (polish-size scenarios): [S][CW] doubles + flags
   int CW = 0;
   double *d_cache = nullptr;
@@ -5272,7 +5356,10 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     using I2 = std::integral_constant<int, 2>;
     using I4 = std::integral_constant<int, 4>;
     using I8 = std::integral_constant<int, 8>;
-    switch (geom) {
+    int gsel = geom;
+    if (gsel == 41 && launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a)) gsel = 0;
+    switch (gsel) {
+      case 0: break;
       case 42: launch_as(I4{}, I2{}); break;
       case 81: launch_as(I8{}, I1{}); break;
       case 22: launch_as(I2{}, I2{}); break;
@@ -5391,6 +5478,7 @@ int ph_batch_solve_summary(ph_batch_t b, int64_t *out) {
 
 int ph_loop_reset(ph_batch_t b, int32_t start_iter, int32_t iter_limit, double convthresh) {
   if (!b || start_iter < 0 || iter_limit < 0) return fail(PH_EINVAL, "ph_loop_reset: bad arguments");
+  b->fused_ran = false;
   LoopCtl h;
   std::memset(&h, 0, sizeof(h));
   h.iter = start_iter;
@@ -5691,6 +5779,11 @@ static bool fused_ok(ph_batch *b, size_t *fin_lds, int *has_md) {
   }
   if (t > 64 * 1024) return false;  // (a big tail carve would cost the polish blocks' occupancy)
   *fin_lds = t;
+  if (const char *v = std::getenv("PHGPU_VERBOSE"); v && std::atoi(v) != 0 && !b->fin_attr) {
+    std::fprintf(stderr, "phgpu fused pass: LDS %zu B (polish %zu, tail %zu, rescue %d)\n", t, polish_lds_bytes(b),
+                 *has_md ? std::max(solve_lds_bytes(b), b->mid_plds_bytes) : solve_lds_bytes(b), *has_md);
+    b->fin_attr = true;
+  }
   return true;
 }
 
@@ -5699,6 +5792,7 @@ static bool fused_ok(ph_batch *b, size_t *fin_lds, int *has_md) {
 // when `u_next` the next pass's update_w_conv).
 static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds, int has_md) {
   const ph_loop_pass_args &p = b->pass;
+  b->fused_ran = true;
   if (first)
     if (int rc = launch_update_w_conv(b, p.x, p.sums, p.G, p.gid, p.rho, p.w_coeff, p.xbar, p.xsqbar, p.W,
                                       p.absdiff, p.wconv, p.conv_hist, nullptr))
@@ -5729,13 +5823,13 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
     b->ev_used += 4;
     HIP_OK(hipEventRecord(tev[0], b->stream));
   }
-  {
+  if (!launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a)) {
     constexpr int WPB = 4;
     const size_t as_lds = sizeof(double) * WPB * ((size_t)b->CW + 4 * b->n + 3 * b->m + WAVE);
     hipLaunchKernelGGL((active_set_kernel<WPB, 1>), dim3((b->S + WPB - 1) / WPB), dim3(WPB * WAVE), as_lds,
                        b->stream, a);
-    HIP_OK(hipGetLastError());
   }
+  HIP_OK(hipGetLastError());
   if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
   FinArgs f;
   f.xa = b->loop_xa;
@@ -5772,11 +5866,7 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
   f.prof = a.prof;  // (ph_debug_prof on: stamps; the polish's own clocks off)
   a.prof = nullptr;
   DISPATCH_EXT(64, 1, b->ext, {
-    if (!b->fin_attr && fin_lds > 64 * 1024) {
-      HIP_OK(hipFuncSetAttribute((const void *)finish_kernel<E_>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)fin_lds));
-      b->fin_attr = true;
-    }
+    if (fin_lds > 64 * 1024) return fail(PH_EINVAL, "finish_kernel: LDS past 64 KB");
     hipLaunchKernelGGL((finish_kernel<E_>), dim3(f.np + f.nsum + f.nu), dim3(WAVE), fin_lds, b->stream, a, b->md,
                        f);
   });
@@ -5867,6 +5957,8 @@ int ph_loop_run(ph_batch_t b, int32_t iters) {
   }
   return PH_OK;
 }
+
+int ph_loop_fused(ph_batch_t b) { return b && b->fused_ran ? 1 : 0; }
 
 int ph_loop_status(ph_batch_t b, int64_t *out) {
   if (!b || !out) return fail(PH_EINVAL, "ph_loop_status: bad arguments");

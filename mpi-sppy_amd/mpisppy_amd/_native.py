@@ -79,6 +79,7 @@ SIGNATURES = [
     ("ph_loop_pass", _c_int, [_c_ptr]),
     ("ph_loop_run", _c_int, [_c_ptr, _c_int]),
     ("ph_loop_persistent", _c_int, [_c_ptr]),
+    ("ph_loop_fused", _c_int, [_c_ptr]),
     ("ph_loop_read_timing", _c_int, [_c_ptr, _c_ptr]),
     ("ph_batch_set_timing", _c_int, [_c_ptr, _c_int]),
     ("ph_batch_read_timing", _c_int, [_c_ptr, _c_ptr]),

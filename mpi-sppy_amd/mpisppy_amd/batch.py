@@ -356,6 +356,10 @@ class DeviceBatch:
         """True when loop_run takes the persistent path for the bound pass."""
         return bool(self.lib.ph_loop_persistent(self.handle))
 
+    def loop_fused(self):
+        """True when a loop_run since the last loop_reset ran the fused two-launch pass."""
+        return bool(self.lib.ph_loop_fused(self.handle))
+
     def loop_read_timing(self):
         """(loop_kernel launches, their total ms, passes they ran) while timing."""
         out = np.zeros(3, dtype=np.float64)

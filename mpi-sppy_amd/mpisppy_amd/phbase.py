@@ -759,7 +759,7 @@ class PHBase(SPBase):
             self._create_solvers()
         kw = self._solve_kwargs(self.current_solver_options)
         b = self.batch
-        chunk = int(chunk or self.PHoptions.get("device_loop_chunk", 16))
+        chunk = int(chunk or self.PHoptions.get("device_loop_chunk", 64))
         if self.conv_hist is None or self.conv_hist.numel() < max(iter_limit, 1):
             old = self.conv_hist
             size = max(iter_limit, 1024, 0 if old is None else 2 * old.numel())

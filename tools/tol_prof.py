@@ -16,7 +16,7 @@ from mpisppy_amd.opt.ph import PH  # noqa: E402
 from mpisppy_amd.examples import farmer  # noqa: E402
 
 S = int(sys.argv[1])
-chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 opts = {"solvername": "mi355x_pdhg", "PHIterLimit": 5000, "defaultPHrho": 1.0,
         "convthresh": 1e-4, "verbose": False, "display_progress": False,
         "iter0_solver_options": {}, "iterk_solver_options": {}, "device_loop_graphs": False,
