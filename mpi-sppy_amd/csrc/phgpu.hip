@@ -14,6 +14,7 @@
 //  * the nonanticipativity kernels (xbar sums, W update, convergence sums)
 //    stream the scenario-fastest [k][s] arrays with coalesced FP64 loads.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <type_traits>
 #include <cstdlib>
 
@@ -2091,7 +2092,12 @@ __global__ void __launch_bounds__(ASG_WPB * WAVE) active_set_g_kernel(SolveArgs 
 
 // active_set_g_kernel when the scenario fits 32 lanes (PHGPU_AS_GROUPED=0:
 // active_set_kernel, A/B hook); returns false when it does not apply.
-static bool launch_as_grouped(int n, int m, int CW, int nnz, int S, hipStream_t st, const SolveArgs &a) {
+// e0 / e1: the launch's own start / stop events (hipExtLaunchKernel: the
+// dispatch's timestamps, no marker packets between the kernels), or null.
+static hipError_t g_as_err = hipSuccess;  // (the last grouped launch's status: launch_as_grouped callers check it)
+static bool launch_as_grouped(int n, int m, int CW, int nnz, int S, hipStream_t st, const SolveArgs &a,
+                              hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+  g_as_err = hipSuccess;
   static const int env = [] {
     const char *e = std::getenv("PHGPU_AS_GROUPED");
     return e && *e ? std::atoi(e) : 1;
@@ -2101,10 +2107,11 @@ static bool launch_as_grouped(int n, int m, int CW, int nnz, int S, hipStream_t 
   const size_t lds = sizeof(double) * ASG_WPB * asg_wave_doubles(CW, n, m, nnz, LPS);
   if (lds > 64 * 1024) return false;
   const int per_block = ASG_WPB * NG;
-  if (LPS == 16)
-    hipLaunchKernelGGL(active_set_g_kernel<16>, dim3((S + per_block - 1) / per_block), dim3(ASG_WPB * WAVE), lds, st, a);
-  else
-    hipLaunchKernelGGL(active_set_g_kernel<32>, dim3((S + per_block - 1) / per_block), dim3(ASG_WPB * WAVE), lds, st, a);
+  const void *kf = LPS == 16 ? (const void *)active_set_g_kernel<16> : (const void *)active_set_g_kernel<32>;
+  SolveArgs ac = a;
+  void *args[1] = {&ac};
+  g_as_err = hipExtLaunchKernel(kf, dim3((S + per_block - 1) / per_block), dim3(ASG_WPB * WAVE), args, lds, st, e0,
+                                e1, 0);
   return true;
 }
 
@@ -5357,7 +5364,10 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     using I4 = std::integral_constant<int, 4>;
     using I8 = std::integral_constant<int, 8>;
     int gsel = geom;
-    if (gsel == 41 && launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a)) gsel = 0;
+    if (gsel == 41 && launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a)) {
+      HIP_OK(g_as_err);
+      gsel = 0;
+    }
     switch (gsel) {
       case 0: break;
       case 42: launch_as(I4{}, I2{}); break;
@@ -5821,16 +5831,19 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
     }
     tev = &b->ev[b->ev_used];
     b->ev_used += 4;
-    HIP_OK(hipEventRecord(tev[0], b->stream));
   }
-  if (!launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a)) {
+  // (timing: each launch carries its own start / stop events)
+  if (!launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a, tev ? tev[0] : nullptr,
+                         tev ? tev[1] : nullptr)) {
     constexpr int WPB = 4;
     const size_t as_lds = sizeof(double) * WPB * ((size_t)b->CW + 4 * b->n + 3 * b->m + WAVE);
+    if (tev) HIP_OK(hipEventRecord(tev[0], b->stream));
     hipLaunchKernelGGL((active_set_kernel<WPB, 1>), dim3((b->S + WPB - 1) / WPB), dim3(WPB * WAVE), as_lds,
                        b->stream, a);
+    if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
   }
+  HIP_OK(g_as_err);
   HIP_OK(hipGetLastError());
-  if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
   FinArgs f;
   f.xa = b->loop_xa;
   f.C = (b->S + FIN_CHUNK - 1) / FIN_CHUNK;
@@ -5867,14 +5880,11 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
   a.prof = nullptr;
   DISPATCH_EXT(64, 1, b->ext, {
     if (fin_lds > 64 * 1024) return fail(PH_EINVAL, "finish_kernel: LDS past 64 KB");
-    hipLaunchKernelGGL((finish_kernel<E_>), dim3(f.np + f.nsum + f.nu), dim3(WAVE), fin_lds, b->stream, a, b->md,
-                       f);
+    void *args[3] = {&a, &b->md, &f};
+    HIP_OK(hipExtLaunchKernel((const void *)finish_kernel<E_>, dim3(f.np + f.nsum + f.nu), dim3(WAVE), args,
+                              fin_lds, b->stream, tev ? tev[2] : nullptr, tev ? tev[3] : nullptr, 0));
   });
   HIP_OK(hipGetLastError());
-  if (tev) {
-    HIP_OK(hipEventRecord(tev[2], b->stream));
-    HIP_OK(hipEventRecord(tev[3], b->stream));
-  }
   return PH_OK;
 }
 

@@ -47,8 +47,9 @@ _INST = re.compile(r"::(\w+\s*<[^>]*>)")
 
 WORKLOADS = {
     "farmer10k_c1": {"scenarios_per_rank": 10000, "crops_multiplier": 1,
-                     "require": {"active_set_kernel": None}, "forbid": ["mid_kernel", "mid_polish_kernel"],
-                     "once_per_solve": ["active_set_kernel"]},
+                     "require": {}, "require_any": ["active_set_kernel", "active_set_g_kernel"],
+                     "forbid": ["mid_kernel", "mid_polish_kernel"],
+                     "once_per_solve": ["active_set_kernel", "active_set_g_kernel"]},
     "farmer10k_c100": {"scenarios_per_rank": 10000, "crops_multiplier": 100,
                        "require": {"mid_kernel": "mid_kernel<512, 3, 2>",
                                    "mid_polish_kernel": "mid_polish_kernel<512, 3, 2>"},
@@ -87,7 +88,10 @@ def _rows(d, pattern):
 def _window(rows, window):
     """(first, last] dispatch ids of the window: the last `window` solve
     calls, or with window "first" the process's first solve call (Iter0)."""
-    summ = sorted({int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "summary_kernel"})
+    # a solve call ends with summary_kernel, or (the fused single-rank
+    # pass, round 5) with finish_kernel
+    summ = sorted({int(r["Dispatch_Id"]) for r in rows
+                   if short(r["Kernel_Name"]) in ("summary_kernel", "finish_kernel")})
     if window == "first":
         if not summ:
             raise SystemExit("pmc_summary: no solve call recorded")
@@ -123,11 +127,13 @@ def validate(tag, res, inst):
         if want is not None and inst.get(k) != {want}:
             raise SystemExit(f"pmc_summary: workload {tag} needs only {want}; the window holds "
                              f"{sorted(inst.get(k, []))}")
+    if w.get("require_any") and not any(k in ks for k in w["require_any"]):
+        raise SystemExit(f"pmc_summary: workload {tag} needs one of {w['require_any']}; found {sorted(ks)}")
     for k in w["forbid"]:
         if k in ks:
             raise SystemExit(f"pmc_summary: workload {tag}: {k} in the window belongs to another config")
     for k in w["once_per_solve"]:
-        if ks[k]["launches_per_solve"] != 1.0:
+        if k in ks and ks[k]["launches_per_solve"] != 1.0:
             raise SystemExit(f"pmc_summary: workload {tag}: {k} at {ks[k]['launches_per_solve']} "
                              "launches per solve (a window of another config's solves)")
 
