@@ -5578,6 +5578,9 @@ int ph_loop_backup_status(ph_batch_t b, const int32_t *status, int32_t *status_s
   return PH_OK;
 }
 
+static bool fused_ok(ph_batch *b, size_t *fin_lds, int *has_md, bool ranks_ok);
+static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds, int has_md);
+
 // update_w_conv_kernel with KL nonant lanes per scenario by the nonant count.
 static int launch_update_w_conv(ph_batch *b, const double *x, const double *sums, int32_t G,
                                 const int32_t *gid, const double *rho, const double *w_coeff,
@@ -5666,6 +5669,11 @@ int ph_loop_pass(ph_batch_t b) {
                        (const int32_t *)p.status, p.status_save, (const double *)p.dbound,
                        p.dbound_save, b->S);
     HIP_OK(hipGetLastError());
+    // the solve as the fused pass's two launches (the next Update_W waits for
+    // the allreduce: not in the launch)
+    size_t fin_lds = 0;
+    int has_md = 0;
+    if (fused_ok(b, &fin_lds, &has_md, true)) return loop_pass_fused(b, false, false, fin_lds, has_md);
   }
   return ph_pdhg_solve(b, p.W, p.rho, p.xbar, p.w_on, p.prox_on, p.x, p.y, p.omega, p.status,
                        p.iters, p.pobj, p.dbound, &p.opts);
@@ -5767,13 +5775,13 @@ int ph_loop_read_timing(ph_batch_t b, double *out) {
 // one-wave cached warm solve, the device loop's Compute_Xbar sums bound to
 // this pass, not under stream capture (a captured chunk replays its first
 // pass's update_w_conv), the tail's LDS small (PHGPU_FUSED=0: off, A/B hook).
-static bool fused_ok(ph_batch *b, size_t *fin_lds, int *has_md) {
+static bool fused_ok(ph_batch *b, size_t *fin_lds, int *has_md, bool ranks_ok) {
   static const int env = [] {
     const char *e = std::getenv("PHGPU_FUSED");
     return e && *e ? std::atoi(e) : 1;
   }();
   const ph_loop_pass_args &p = b->pass;
-  if (!env || p.conv_part || b->mid || !polish_fits(b) || !b->d_sb || !b->d_cache || !p.opts.polish ||
+  if (!env || (p.conv_part && !ranks_ok) || b->mid || !polish_fits(b) || !b->d_sb || !b->d_cache || !p.opts.polish ||
       !p.opts.warm_start || b->K <= 0 || p.G <= 0 || b->loop_xa.G != p.G || b->loop_xa.C <= 0 ||
       b->loop_xa.x != p.x || b->loop_xa.out != p.sums)
     return false;
@@ -5897,7 +5905,7 @@ int ph_loop_run(ph_batch_t b, int32_t iters) {
   if (!persist) {  // the per-pass kernels
     size_t fin_lds = 0;
     int has_md = 0;
-    if (fused_ok(b, &fin_lds, &has_md)) {  // three launches per pass -> two
+    if (fused_ok(b, &fin_lds, &has_md, false)) {  // three launches per pass -> two
       for (int i = 0; i < iters; ++i)
         if (int rc = loop_pass_fused(b, i == 0, i + 1 < iters, fin_lds, has_md)) return rc;
       return PH_OK;
@@ -5968,7 +5976,7 @@ int ph_loop_run(ph_batch_t b, int32_t iters) {
   return PH_OK;
 }
 
-int ph_loop_fused(ph_batch_t b) { return b && b->fused_ran ? 1 : 0; }
+int ph_loop_fused(ph_batch_t b) { return b && b->fused_ran ? 1 : 0; }  // (one rank or several)
 
 int ph_loop_status(ph_batch_t b, int64_t *out) {
   if (!b || !out) return fail(PH_EINVAL, "ph_loop_status: bad arguments");
