@@ -4479,6 +4479,18 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   return PH_OK;
 }
 
+__global__ void loop_reset_kernel(LoopCtl *c, int32_t start_iter, int32_t iter_limit, double convthresh) {
+  LoopCtl h;
+  std::memset(&h, 0, sizeof(h));
+  h.iter = start_iter;
+  h.limit = iter_limit;
+  h.thresh = convthresh;
+  // begin the first iteration (the post-solve kernel begins the others)
+  if (h.iter >= h.limit) h.stop = 2;
+  else h.iter += 1;
+  *c = h;
+}
+
 extern "C" {
 
 const char *ph_version(void) { return PHGPU_VERSION; }
@@ -5489,16 +5501,11 @@ int ph_batch_solve_summary(ph_batch_t b, int64_t *out) {
 int ph_loop_reset(ph_batch_t b, int32_t start_iter, int32_t iter_limit, double convthresh) {
   if (!b || start_iter < 0 || iter_limit < 0) return fail(PH_EINVAL, "ph_loop_reset: bad arguments");
   b->fused_ran = false;
-  LoopCtl h;
-  std::memset(&h, 0, sizeof(h));
-  h.iter = start_iter;
-  h.limit = iter_limit;
-  h.thresh = convthresh;
-  // begin the first iteration (the post-solve kernel begins the others)
-  if (h.iter >= h.limit) h.stop = 2;
-  else h.iter += 1;
-  HIP_OK(hipMemcpyAsync(b->d_ctl, &h, sizeof(h), hipMemcpyHostToDevice, b->stream));
-  HIP_OK(hipStreamSynchronize(b->stream));  // h is on this stack frame
+  // (a one-thread kernel writes the state: no host staging copy and stream
+  // synchronisation before the loop's first launch)
+  hipLaunchKernelGGL(loop_reset_kernel, dim3(1), dim3(1), 0, b->stream, b->d_ctl, start_iter, iter_limit,
+                     convthresh);
+  HIP_OK(hipGetLastError());
   b->st_sp = b->st_pol = b->st_hit = 0;  // the counters restart (obs_* carry over)
   return PH_OK;
 }
