@@ -2098,10 +2098,8 @@ static hipError_t g_as_err = hipSuccess;  // (the last grouped launch's status: 
 static bool launch_as_grouped(int n, int m, int CW, int nnz, int S, hipStream_t st, const SolveArgs &a,
                               hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
   g_as_err = hipSuccess;
-  static const int env = [] {
-    const char *e = std::getenv("PHGPU_AS_GROUPED");
-    return e && *e ? std::atoi(e) : 1;
-  }();
+  const char *ge = std::getenv("PHGPU_AS_GROUPED");  // (read per call: the tests compare both forms)
+  const int env = ge && *ge ? std::atoi(ge) : 1;
   if (!env || n > 32 || m > 32) return false;
   const int LPS = (n <= 16 && m <= 16) ? 16 : 32, NG = 64 / LPS;
   const size_t lds = sizeof(double) * ASG_WPB * asg_wave_doubles(CW, n, m, nnz, LPS);
@@ -5321,10 +5319,8 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
   const size_t lds = solve_lds_bytes(b);
   if (lds > 160 * 1024) return fail(PH_EINVAL, "ph_pdhg_solve: scenario does not fit in LDS");
   if (int rc = ensure_pdhg_grid(b, lds)) return rc;
-  static const int prime_env = [] {  // PHGPU_PRIME=0: off (A/B hook)
-    const char *e = std::getenv("PHGPU_PRIME");
-    return e && *e ? std::atoi(e) : 1;
-  }();
+  const char *pe = std::getenv("PHGPU_PRIME");  // PHGPU_PRIME=0: off (A/B hook; read per call)
+  const int prime_env = pe && *pe ? std::atoi(pe) : 1;
   if (prime_env && a.cache && a.warm && !b->primed && !b->loop_on && b->S > PRIME_REPS) {
     // (hints of the first cached solve; needs the hint arrays in a)
     SolveArgs ap = a;
@@ -5783,10 +5779,8 @@ int ph_loop_read_timing(ph_batch_t b, double *out) {
 // this pass, not under stream capture (a captured chunk replays its first
 // pass's update_w_conv), the tail's LDS small (PHGPU_FUSED=0: off, A/B hook).
 static bool fused_ok(ph_batch *b, size_t *fin_lds, int *has_md, bool ranks_ok) {
-  static const int env = [] {
-    const char *e = std::getenv("PHGPU_FUSED");
-    return e && *e ? std::atoi(e) : 1;
-  }();
+  const char *fe = std::getenv("PHGPU_FUSED");  // (read per call: the tests compare both forms)
+  const int env = fe && *fe ? std::atoi(fe) : 1;
   const ph_loop_pass_args &p = b->pass;
   if (!env || (p.conv_part && !ranks_ok) || b->mid || !polish_fits(b) || !b->d_sb || !b->d_cache || !p.opts.polish ||
       !p.opts.warm_start || b->K <= 0 || p.G <= 0 || b->loop_xa.G != p.G || b->loop_xa.C <= 0 ||

@@ -1220,3 +1220,64 @@ def test_supernodal_factor_on_device_matches_sparse_kkt(kind, tmp_path):
     d = lines[-1]
     assert d["residual"] <= 1e-11 * max(1.0, d["znorm"]), d
     assert d["rerun_diff"] == 0.0, d   # deterministic
+
+
+def _farmer_loop(S, passes, env, monkeypatch, thresh=-1.0):
+    """Iter0 + run_device_loop(0, passes) of farmer S with the environment
+    `env` set; (iterations, stop, conv history, xbar, W, x, Iter0 bound,
+    fused form ran)."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ph = PH(dict(_opts(PHIterLimit=passes, convthresh=thresh)), [f"scen{i}" for i in range(S)],
+            farmer.scenario_creator)
+    ph.PH_Prep()
+    ph.subproblem_creation()
+    ph._create_solvers()
+    tb = ph.Iter0()
+    stop, it = ph.run_device_loop(0, passes, thresh, chunk=16)
+    fused = ph.batch.loop_fused()
+    return (it, stop, ph.conv_hist[:it].cpu().numpy().copy(), ph.xbar.cpu().numpy().copy(),
+            ph.W.cpu().numpy().copy(), ph.batch.x.cpu().numpy().copy(), tb, fused)
+
+
+def test_fused_pass_matches_five_launch_chain(monkeypatch):
+    """The fused per-pass form (active_set_g_kernel + finish_kernel: polish,
+    tail, Compute_Xbar sums, counters, the next pass's Update_W and stop
+    test in one launch) against the five-launch chain from PH iteration 1
+    (many misses and tails): same iterations, conv history, x-bar, W and x
+    up to the sums' order (Compute_Xbar in 256- vs 2048-scenario chunks)."""
+    base = {"PHGPU_PERSIST": "0", "PHGPU_PRIME": "0"}
+    p = _farmer_loop(1000, 40, {**base, "PHGPU_FUSED": "1"}, monkeypatch)
+    q = _farmer_loop(1000, 40, {**base, "PHGPU_FUSED": "0"}, monkeypatch)
+    assert p[7] and not q[7], "the fused form did not run (or ran when off)"
+    assert p[0] == q[0] == 40 and p[1] == q[1]
+    assert np.allclose(p[2], q[2], rtol=1e-8, atol=1e-12)
+    for a, b_ in zip(p[3:6], q[3:6]):
+        assert _rel(a, b_) < 5e-8
+
+
+def test_grouped_cached_maps_bitwise_one_wave(monkeypatch):
+    """active_set_g_kernel (four scenarios per wave, as_evalg) takes the
+    same decisions and writes the same solutions as active_set_kernel (one
+    scenario per wave, as_eval): bitwise equal x over 30 PH iterations of
+    the five-launch chain."""
+    base = {"PHGPU_PERSIST": "0", "PHGPU_PRIME": "0", "PHGPU_FUSED": "0"}
+    p = _farmer_loop(300, 30, {**base, "PHGPU_AS_GROUPED": "1"}, monkeypatch)
+    q = _farmer_loop(300, 30, {**base, "PHGPU_AS_GROUPED": "0"}, monkeypatch)
+    assert p[0] == q[0]
+    assert np.array_equal(p[5], q[5]) and np.array_equal(p[4], q[4])
+
+
+def test_seeded_iter0_matches_unseeded(monkeypatch):
+    """Iter0 with hints seeded from PDHG representatives (prime_hints) and
+    without: every LP optimal, the same trivial bound and first-stage
+    solutions (the farmer LPs' optima are unique) and the same PH
+    trajectory afterwards."""
+    p = _farmer_loop(1000, 10, {"PHGPU_PRIME": "1"}, monkeypatch)
+    q = _farmer_loop(1000, 10, {"PHGPU_PRIME": "0"}, monkeypatch)
+    assert abs(p[6] - q[6]) <= 1e-9 * abs(q[6])
+    assert p[0] == q[0]
+    for a, b_ in zip(p[3:6], q[3:6]):
+        assert _rel(a, b_) < 1e-7
