@@ -2029,7 +2029,8 @@ __global__ void __launch_bounds__(WPB * WAVE) active_set_kernel(SolveArgs a) {
 // The cached maps of 64 / LPS scenarios per wave (as_evalg: LPS lanes per
 // scenario when n, m <= LPS), four waves per block: F2 evaluates four
 // scenarios per wave in one pass of the chain active_set_kernel runs once
-// per scenario (bitwise the same checks).  Per wave in LDS: the scenarios'
+// per scenario (the same checks; the clipped case's products and the sums
+// in group order).  Per wave in LDS: the scenarios'
 // entries, static blocks and values, the clipped case's scratch, the entry
 // flags.
 constexpr int ASG_WPB = 4;

@@ -1258,16 +1258,20 @@ def test_fused_pass_matches_five_launch_chain(monkeypatch):
         assert _rel(a, b_) < 5e-8
 
 
-def test_grouped_cached_maps_bitwise_one_wave(monkeypatch):
-    """active_set_g_kernel (four scenarios per wave, as_evalg) takes the
-    same decisions and writes the same solutions as active_set_kernel (one
-    scenario per wave, as_eval): bitwise equal x over 30 PH iterations of
-    the five-launch chain."""
+def test_grouped_cached_maps_match_one_wave(monkeypatch):
+    """active_set_g_kernel (four scenarios per wave, as_evalg) against
+    active_set_kernel (one scenario per wave, as_eval) over 30 PH iterations
+    of the five-launch chain: the same iterations, x-bar, W and x to the
+    solves' 1e-9 KKT tolerance amplified over the iterations (the group's
+    clipped-case products and sums are ordered differently from the
+    one-wave form's, so a check at the tolerance's edge can fall the other
+    way and a scenario be polished instead of mapped)."""
     base = {"PHGPU_PERSIST": "0", "PHGPU_PRIME": "0", "PHGPU_FUSED": "0"}
     p = _farmer_loop(300, 30, {**base, "PHGPU_AS_GROUPED": "1"}, monkeypatch)
     q = _farmer_loop(300, 30, {**base, "PHGPU_AS_GROUPED": "0"}, monkeypatch)
     assert p[0] == q[0]
-    assert np.array_equal(p[5], q[5]) and np.array_equal(p[4], q[4])
+    for a, b_ in zip(p[3:6], q[3:6]):
+        assert _rel(a, b_) < 5e-8
 
 
 def test_seeded_iter0_matches_unseeded(monkeypatch):
