@@ -8,7 +8,7 @@ mkdir -p $O
 cd $R
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -v --timeout 400 --timeout-method thread -m gpu tests/test_gpu_parity.py \
-  -k "c100 or mid or sslp or fused_pass or grouped_cached or seeded_iter0" > $O/pytest_r05_f3pk.log 2>&1; rc=$?
+  -k "grouped_cached" > $O/pytest_r05_f3pk.log 2>&1; rc=$?
 grep -E "FAILED|ERROR|passed|failed" $O/pytest_r05_f3pk.log | tail -8
 [ $rc -eq 0 ] || { grep -v "^frame" $O/pytest_r05_f3pk.log | tail -40; exit $rc; }
 timeout -k 10 300 python -u bench.py --only f3 --no-cpu-baseline --tol-run 0 > $O/f3pk.json 2> $O/f3pk.err || { echo "f3 failed"; tail -20 $O/f3pk.err; exit 1; }
