@@ -4174,17 +4174,26 @@ static int check_dev(const int32_t (&e)[4]) {
 // The LDL' polish's knobs (measurement hooks, environment variables read
 // at batch creation): regularisation, PDAS rounds, pinned rows, refinement
 // tolerance.
+// PDAS rounds of one mid-size / big polish (PHGPU_MID_POLISH_ROUNDS
+// overrides).  Prox terms on many columns move the active set over many
+// columns per PH iteration: F3 (K/n = 0.25) fails 1,785 of 10k warm
+// polishes at 6 rounds in PH iteration 6 and 13 at 10 (that pass 14.7 ->
+// 10.1 ms); sslp (K/n = 0.02) fails the same ~980 at 6, 10 or 16 rounds
+// (its LP relaxation's degenerate sets, not the round limit) and only pays
+// for the extra rounds (profiles/r05/mid_rounds_sweep.txt).  The big path
+// and the one-wave batches' rescue polish keep 6 (not measured at more).
+static int polish_rounds(const ph_batch *b) {
+  if (const char *e = std::getenv("PHGPU_MID_POLISH_ROUNDS")) return std::max(1, std::atoi(e));
+  return (b->mid && !b->big && b->K > 0 && 10 * b->K >= b->n) ? 10 : MID_POLISH_ROUNDS;
+}
+
 static int kkt_knobs(ph_batch *b) {
   {  // PHGPU_KKT_DELTA: measurement hook for the polish regularisation
     const char *e = std::getenv("PHGPU_KKT_DELTA");
     b->md.delta = e ? std::atof(e) : KKT_DELTA;
   }
-  {  // PHGPU_MID_POLISH_ROUNDS: PDAS rounds of one mid-size polish
-    const char *e = std::getenv("PHGPU_MID_POLISH_ROUNDS");
-    if (e) {
-      const int r = std::max(1, std::atoi(e));
-      HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_polish_rounds), &r, sizeof(r)));
-    }
+  {  // PDAS rounds of one polish (the K-dependent default: polish_rounds)
+    b->md.rounds = polish_rounds(b);
   }
   {  // PHGPU_BIG_POLISH_ROUNDS: PDAS rounds of one big-path polish
     const char *e = std::getenv("PHGPU_BIG_POLISH_ROUNDS");
@@ -4703,6 +4712,7 @@ int ph_batch_set_nonants(ph_batch_t b, int32_t K, const int32_t *nonant_col) {
   HIP_OK(hipMemcpyAsync(b->d_nonant_col, nonant_col, sizeof(int32_t) * (K ? K : 0), hipMemcpyHostToDevice, b->stream));
   HIP_OK(hipMemcpyAsync(b->d_slot_of_col, slot.data(), sizeof(int32_t) * b->n, hipMemcpyHostToDevice, b->stream));
   b->K = K;
+  b->md.rounds = polish_rounds(b);  // (K-dependent)
   // active-set cache for scenarios the one-wave polish covers
   for (void *p : {(void *)b->d_cache, (void *)b->d_cache_ok, (void *)b->d_hint,
                   (void *)b->d_hint_ok, (void *)b->d_wl, (void *)b->d_wl2})
