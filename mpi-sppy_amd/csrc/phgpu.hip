@@ -2095,10 +2095,10 @@ __global__ void __launch_bounds__(ASG_WPB * WAVE) active_set_g_kernel(SolveArgs 
 // active_set_kernel, A/B hook); returns false when it does not apply.
 // e0 / e1: the launch's own start / stop events (hipExtLaunchKernel: the
 // dispatch's timestamps, no marker packets between the kernels), or null.
-static hipError_t g_as_err = hipSuccess;  // (the last grouped launch's status: launch_as_grouped callers check it)
+// *err: the launch's status (callers check it).
 static bool launch_as_grouped(int n, int m, int CW, int nnz, int S, hipStream_t st, const SolveArgs &a,
-                              hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
-  g_as_err = hipSuccess;
+                              hipError_t *err, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+  *err = hipSuccess;
   const char *ge = std::getenv("PHGPU_AS_GROUPED");  // (read per call: the tests compare both forms)
   const int env = ge && *ge ? std::atoi(ge) : 1;
   if (!env || n > 32 || m > 32) return false;
@@ -2109,8 +2109,8 @@ static bool launch_as_grouped(int n, int m, int CW, int nnz, int S, hipStream_t 
   const void *kf = LPS == 16 ? (const void *)active_set_g_kernel<16> : (const void *)active_set_g_kernel<32>;
   SolveArgs ac = a;
   void *args[1] = {&ac};
-  g_as_err = hipExtLaunchKernel(kf, dim3((S + per_block - 1) / per_block), dim3(ASG_WPB * WAVE), args, lds, st, e0,
-                                e1, 0);
+  *err = hipExtLaunchKernel(kf, dim3((S + per_block - 1) / per_block), dim3(ASG_WPB * WAVE), args, lds, st, e0,
+                             e1, 0);
   return true;
 }
 
@@ -5383,8 +5383,9 @@ int ph_pdhg_solve(ph_batch_t b, const double *W, const double *rho, const double
     using I4 = std::integral_constant<int, 4>;
     using I8 = std::integral_constant<int, 8>;
     int gsel = geom;
-    if (gsel == 41 && launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a)) {
-      HIP_OK(g_as_err);
+    hipError_t ae = hipSuccess;
+    if (gsel == 41 && launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a, &ae)) {
+      HIP_OK(ae);
       gsel = 0;
     }
     switch (gsel) {
@@ -5513,6 +5514,9 @@ int ph_loop_reset(ph_batch_t b, int32_t start_iter, int32_t iter_limit, double c
   hipLaunchKernelGGL(loop_reset_kernel, dim3(1), dim3(1), 0, b->stream, b->d_ctl, start_iter, iter_limit,
                      convthresh);
   HIP_OK(hipGetLastError());
+  // (finish_kernel's counters: zero after every complete launch; a launch
+  // that aborted on a wait budget leaves them set)
+  if (b->d_fin) HIP_OK(hipMemsetAsync(b->d_fin, 0, FIN_WORDS * sizeof(int32_t), b->stream));
   b->st_sp = b->st_pol = b->st_hit = 0;  // the counters restart (obs_* carry over)
   return PH_OK;
 }
@@ -5853,7 +5857,8 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
     b->ev_used += 4;
   }
   // (timing: each launch carries its own start / stop events)
-  if (!launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a, tev ? tev[0] : nullptr,
+  hipError_t ae = hipSuccess;
+  if (!launch_as_grouped(b->n, b->m, b->CW, b->nnz, b->S, b->stream, a, &ae, tev ? tev[0] : nullptr,
                          tev ? tev[1] : nullptr)) {
     constexpr int WPB = 4;
     const size_t as_lds = sizeof(double) * WPB * ((size_t)b->CW + 4 * b->n + 3 * b->m + WAVE);
@@ -5862,7 +5867,7 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
                        b->stream, a);
     if (tev) HIP_OK(hipEventRecord(tev[1], b->stream));
   }
-  HIP_OK(g_as_err);
+  HIP_OK(ae);
   HIP_OK(hipGetLastError());
   FinArgs f;
   f.xa = b->loop_xa;
