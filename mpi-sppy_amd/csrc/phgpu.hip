@@ -5872,7 +5872,10 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
   FinArgs f;
   f.xa = b->loop_xa;
   f.C = (b->S + FIN_CHUNK - 1) / FIN_CHUNK;
-  f.np = std::min(b->S, 1024);
+  {  // polish blocks (PHGPU_FIN_NP: measurement hook)
+    const char *e = std::getenv("PHGPU_FIN_NP");
+    f.np = std::min(b->S, e && *e ? std::max(64, std::atoi(e)) : 1024);
+  }
   f.tb = std::min(f.np, 64);
   if (has_md && b->md.ws_g) f.tb = std::max(1, std::min(f.tb, b->md.ws_blocks));
   f.nsum = p.G * f.C;
