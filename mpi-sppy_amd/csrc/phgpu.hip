@@ -3131,7 +3131,17 @@ __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, F
     int last = 0;
     if (lane == 0) last = fin_ticket(fin + FIN_SUMT) == f.nsum - 1;
     if (!__shfl(last, 0, WAVE)) return;
-    // the last chunk: the sums in chunk order, the counters, the advance
+    // the last chunk: the sums in chunk order, the advance, the update
+    // blocks released; then the solve's counters (the list counts read
+    // first: the last update block clears them)
+    int nl = 0, c0l = 0, stp = 0, itn = 0, lim = 0;
+    if (lane == 0) {  // (in flight with the partials' loads)
+      nl = min(fin_load(a.wl2_count), S);
+      c0l = list_count(a.wl_count, S, a.err);
+      stp = ctl->stop;
+      itn = ctl->iter;
+      lim = ctl->limit;
+    }
     fin_stage(lds, f.part, 2 * f.nsum, lane);
     for (int gg = lane; gg < G; gg += WAVE) {
       double a0 = 0.0, a1 = 0.0;
@@ -3142,10 +3152,19 @@ __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, F
       pub(xa.out + gg, a0);
       pub(xa.out + G + gg, a1);
     }
+    if (lane == 0) {
+      // loop_advance, stores the update blocks read through atomics
+      if (!stp) {
+        if (itn >= lim) __hip_atomic_store(&ctl->stop, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_store(&ctl->iter, itn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (f.prof) atomicMax(&f.prof[19], wall_clock64());
+      if (f.nu > 0) fin_ticket(fin + FIN_READY);  // (after the sums' and the control's stores: the wave's)
+    }
     // summary_kernel's block 0 over the tail list: (not optimal, iters sum,
     // iters max, polished, cached)
+    nl = __shfl(nl, 0, WAVE);
     unsigned long long v[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
-    const int nl = min(fin_load(a.wl2_count), S);
     for (int q = lane; q < nl; q += WAVE) {
       const int s = fin_load(a.wl2 + q);
       if (s < 0 || s >= S) {
@@ -3169,7 +3188,6 @@ __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, F
         v[i] = i == 2 ? (o > v[i] ? o : v[i]) : v[i] + o;
       }
     if (lane == 0) {
-      const int c0l = list_count(a.wl_count, S, a.err);
       v[3] += (unsigned long long)max(c0l - nl, 0);
       v[4] += (unsigned long long)(S - c0l);
       for (int i = 0; i < 5; ++i) f.summary[i] = v[i];
@@ -3179,16 +3197,7 @@ __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, F
       ctl->acc[3] = v[2] > ctl->acc[3] ? v[2] : ctl->acc[3];
       ctl->acc[4] += v[3];
       ctl->acc[5] += v[4];
-      // loop_advance, stores the update blocks read through atomics
-      const int stp = ctl->stop, itn = ctl->iter;
-      if (!stp) {
-        if (itn >= ctl->limit) __hip_atomic_store(&ctl->stop, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else __hip_atomic_store(&ctl->iter, itn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (f.prof) atomicMax(&f.prof[19], wall_clock64());
-      if (f.nu > 0) {
-        fin_ticket(fin + FIN_READY);  // (after the sums' and the control's stores)
-      } else {  // the launch's counters back to zero
+      if (f.nu == 0) {  // the launch's counters back to zero
         for (int q = 0; q < 8; ++q) __hip_atomic_store(fin + FIN_DONE + 16 * q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(fin + FIN_TAIL, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(fin + FIN_SUMT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
