@@ -5187,7 +5187,8 @@ __global__ void __launch_bounds__(WAVE) prime_hint_kernel(SolveArgs a, int R) {
 }
 
 static int prime_hints(ph_batch *b, SolveArgs a, size_t lds) {
-  const int R = std::min(b->S, PRIME_REPS);
+  const char *re = std::getenv("PHGPU_PRIME_REPS");  // (measurement hook)
+  const int R = std::min(b->S, re && *re ? std::max(1, std::atoi(re)) : PRIME_REPS);
   hipLaunchKernelGGL(prime_list_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_wl, b->d_ctr, b->S, R);
   HIP_OK(hipMemsetAsync(b->d_ctr + 1, 0, sizeof(int32_t), b->stream));  // (pdhg_kernel's queue)
   a.wl = b->d_wl;
