@@ -20,6 +20,7 @@ Rank 0 prints ONE JSON line.  Input data are synthetic farmer instances
 generated exactly as the reference's examples/farmer/farmer.py does.
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -392,6 +393,42 @@ def hbm_config(args, world, farmer, PH, opts):
                                              "from HBM would need -- a work rate, not a measurement"}}
 
 
+def f4_bracket(ph, iters, trivial_bound, ef):
+    """The bracket around the published EF after the bench's PH window (its
+    W and x-bar): post_solve_bound (phbase.py:753-801: W on, prox off, the LP
+    bound) <= EF <= the implementable x-bar objective (every scenario at the
+    consensus first stage, W and prox off: the xhat of
+    extensions/xhatbase.py).  Both are valid at any PH iteration; the EF
+    (-1.334838651e8, paperruns/scripts/farmer/ef_1000_1000.out:183) must lie
+    between them (`ok`)."""
+    _progress("F4 EF bracket (x-bar objective, post_solve_bound)")
+    t0 = time.perf_counter()
+    ph._PHIter = iters
+    ph.conv = float(ph.conv_hist[iters - 1].item()) if iters > 0 else None
+    xb = ph.xbar.view(ph.K, ph.S_loc)[:, 0].cpu().numpy()
+    ph._save_nonants()
+    ph._fix_nonants(xb)
+    kw = ph.solve_loop_launch(solver_options={"pdhg_max_iters": 100000}, dis_W=True, dis_prox=True)
+    ph.solve_loop_finish(kw)
+    xh_ok = bool((ph.batch.status == 0).all().item())
+    wd, pd = ph.W_disabled, ph.prox_disabled
+    ph._disable_W_and_prox()
+    xhat = ph.Eobjective() if xh_ok else None
+    ph.W_disabled, ph.prox_disabled = wd, pd
+    ph._set_flags()
+    ph._restore_nonants()
+    with contextlib.redirect_stdout(sys.stderr):  # (its reference warning: stdout holds the one JSON line)
+        psb = ph.post_solve_bound()
+    torch.cuda.synchronize()
+    out = {"after_ph_iterations": iters, "trivial_bound": trivial_bound, "post_solve_bound": psb,
+           "xbar_objective": xhat, "published_ef": ef, "seconds": round(time.perf_counter() - t0, 2)}
+    if ef is not None:
+        out["ok"] = bool(psb <= ef + 1e-9 * abs(ef) and trivial_bound <= ef + 1e-9 * abs(ef)
+                         and xhat is not None and ef <= xhat + 1e-9 * abs(ef))
+        out["width_rel"] = None if xhat is None else (xhat - psb) / abs(ef)
+    return out
+
+
 def big_config(args, world, farmer, PH, opts):
     """farmer crops_multiplier --f4-crops (1000: n=12,000,
     m=9,001, nnz=27,000 per scenario), --f4-scens scenarios per rank (1000,
@@ -440,6 +477,7 @@ def big_config(args, world, farmer, PH, opts):
     if world > 1:
         dist.all_reduce(d, op=dist.ReduceOp.MAX)
     dt = float(d.item())
+    bracket = f4_bracket(ph, 1 + args.hbm_steps, tb, -1.334838651e8 if (S == 1000 and c == 1000) else None)
     n, m, nnz = b.n, b.m, b.nnz
     bit = 8 * (2 * nnz + 7 * n + 5 * m)
     steps = st[4]
@@ -456,6 +494,7 @@ def big_config(args, world, farmer, PH, opts):
             "ms_per_step": round(dt / args.hbm_steps * 1000.0, 3), "steps": args.hbm_steps,
             "iter0_s": round(t_iter0, 3), "iter0_not_optimal": nonopt0, "trivial_bound": tb,
             "published_ef": -1.334838651e8 if (S == 1000 and c == 1000) else None,
+            "ef_bracket": bracket,
             "pdhg_steps_per_solve": round(steps / max(st[3], 1), 1), "pdhg_steps_max": st[5],
             "polished_per_solve": round(st[6] / max(st[3], 1), 3), "not_optimal_in_window": st[2],
             "roofline": {"bound": "hbm", "kernel": "big_kernel + big_team_kernel (a PDHG phase launch)",

@@ -164,10 +164,6 @@ struct KktSymbolic {
         error = "the KKT factor has more than 2^31 entries";
         return false;
       }
-      if (lists && nc > kMaxContrib) {
-        error = "the KKT factor's update lists exceed 2^28 entries";
-        return false;
-      }
       ncontrib = (long)nc;
     }
     Lcp.assign(N + 1, 0);
@@ -232,8 +228,32 @@ struct KktSymbolic {
     ec1.clear();
     ec2.clear();
     eck.clear();
-    if (lists) {
-    // ---- update lists: entry (r,c) -= L(r,k) D(k) L(c,k) for k < c
+    if (lists && !build_lists()) return false;
+    // ---- A's entries in L
+    apos.resize(nnz);
+    arow.resize(nnz);
+    for (int i = 0; i < m; ++i)
+      for (int p = row_ptr[i]; p < row_ptr[i + 1]; ++p) {
+        const int pj = pos[col_idx[p]], pi = pos[n + i];
+        apos[p] = pj > pi ? entry(pj, pi) : entry(pi, pj);
+        arow[p] = i;
+      }
+    return true;
+  }
+
+  // The update lists of the per-entry factorisation (entry (r,c) -= L(r,k)
+  // D(k) L(c,k) for k < c) from the analysed pattern: a pattern analysed
+  // with lists = false gets them later without a second ordering (the big
+  // path builds them only when its per-entry polish will run).
+  bool build_lists() {
+    if (ncontrib > kMaxContrib) {
+      error = "the KKT factor's update lists exceed 2^28 entries";
+      return false;
+    }
+    auto entry = [&](int r, int c) {
+      const auto b = Lri.begin() + Lcp[c], e = Lri.begin() + Lcp[c + 1];
+      return (int32_t)(std::lower_bound(b, e, r) - Lri.begin());
+    };
     std::vector<int32_t> cnt(nnzL + 1, 0);
     for (int k = 0; k < N; ++k)
       for (int a = Lcp[k]; a < Lcp[k + 1]; ++a)
@@ -244,28 +264,16 @@ struct KktSymbolic {
     ec1.resize(ncontrib);
     ec2.resize(ncontrib);
     eck.resize(ncontrib);
-    {
-      std::vector<int32_t> fill(ecp.begin(), ecp.end() - 1);
-      for (int k = 0; k < N; ++k)
-        for (int a = Lcp[k]; a < Lcp[k + 1]; ++a)
-          for (int b = a + 1; b < Lcp[k + 1]; ++b) {
-            const int e = entry(Lri[b], Lri[a]);
-            const int q = fill[e]++;
-            ec1[q] = b;  // L(r,k)
-            ec2[q] = a;  // L(c,k)
-            eck[q] = k;
-          }
-    }
-    }
-    // ---- A's entries in L
-    apos.resize(nnz);
-    arow.resize(nnz);
-    for (int i = 0; i < m; ++i)
-      for (int p = row_ptr[i]; p < row_ptr[i + 1]; ++p) {
-        const int pj = pos[col_idx[p]], pi = pos[n + i];
-        apos[p] = pj > pi ? entry(pj, pi) : entry(pi, pj);
-        arow[p] = i;
-      }
+    std::vector<int32_t> fill(ecp.begin(), ecp.end() - 1);
+    for (int k = 0; k < N; ++k)
+      for (int a = Lcp[k]; a < Lcp[k + 1]; ++a)
+        for (int b = a + 1; b < Lcp[k + 1]; ++b) {
+          const int e = entry(Lri[b], Lri[a]);
+          const int q = fill[e]++;
+          ec1[q] = b;  // L(r,k)
+          ec2[q] = a;  // L(c,k)
+          eck[q] = k;
+        }
     return true;
   }
 };

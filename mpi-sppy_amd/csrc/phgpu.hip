@@ -1830,9 +1830,11 @@ __device__ __forceinline__ void pend_put(double *pd, int n, int m, int hl, bool 
 // Sum over this lane's group of LPS lanes (16: one DPP row, 32: a half
 // wave), uniform within the group.  The DPP steps stay inside 16-lane rows
 // (after them every lane holds its row's sum); a 32-lane group adds its two
-// row sums.  For a scenario's data in its group's first lanes this adds
-// exactly what wave_sum adds for the same data in lanes 0.. of a wave (the
-// other row sums are zeros there), so the check is bitwise as_eval's.
+// row sums.  The association order is not wave_sum's (DPP row steps, then
+// the row sums, against wave_sum's xor tree over 64 lanes), so the grouped
+// check agrees with as_eval's to rounding, not bitwise: the same accept /
+// reject decisions in the parity runs, x / W / x-bar within 5e-8
+// (test_grouped_cached_maps_bitwise_one_wave's tolerance).
 template <int LPS>
 __device__ __forceinline__ double group_sum(double v) {
   v += dpp_f64<0xB1>(v);
@@ -2988,7 +2990,11 @@ __global__ void __launch_bounds__(1024) summary_kernel(int S, const int32_t *__r
 // tail block's outputs; its done count after it).
 // ------------------------------------------------------------------------
 constexpr int FIN_CHUNK = 256;  // scenarios per sum / update block
-constexpr int FIN_DONE = 0, FIN_TAIL = 128, FIN_SUMT = 144, FIN_READY = 160, FIN_UT = 176, FIN_WORDS = 192;
+// FIN_TPASS: tail blocks that have passed their wait on FIN_DONE (a block
+// that zeroes FIN_DONE first waits for all tb of them: a tail block still
+// polling FIN_DONE would otherwise miss the count and spin to the timeout)
+constexpr int FIN_DONE = 0, FIN_TAIL = 128, FIN_SUMT = 144, FIN_READY = 160, FIN_UT = 176, FIN_TPASS = 192,
+              FIN_WORDS = 208;
 
 struct FinArgs {
   XbarArgs xa;          // the pass's Compute_Xbar sums (xa.out) over its slot ranges; xa.part unused
@@ -3023,6 +3029,31 @@ __device__ __forceinline__ void fin_wait(const int32_t *p, int target, int shard
   }
   __syncthreads();
 }
+// (thread 0 alone) spin until *p >= target, as fin_wait
+__device__ __forceinline__ void fin_wait_lane(const int32_t *p, int target, int32_t *err) {
+  const unsigned long long t0 = wall_clock64();
+  while (fin_load(p) < target) {
+    if (wall_clock64() - t0 > 400000000ull) {
+      dev_fail(err, CHK_BARRIER, target, fin_load(p));
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+// The launch's counters back to zero (thread 0 of the block that is last in
+// its role: every other block of the launch has ticked its last counter, and
+// the tail blocks have passed their wait on FIN_DONE).
+__device__ __forceinline__ void fin_reset(int32_t *fin, int tb, bool with_update, int32_t *err) {
+  fin_wait_lane(fin + FIN_TPASS, tb, err);
+  for (int q = 0; q < 8; ++q) __hip_atomic_store(fin + FIN_DONE + 16 * q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fin + FIN_TAIL, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fin + FIN_SUMT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fin + FIN_TPASS, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (with_update) {
+    __hip_atomic_store(fin + FIN_READY, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(fin + FIN_UT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 __device__ __forceinline__ int fin_ticket(int32_t *p) {  // (thread 0) after the block's publishing stores
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   return __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3050,7 +3081,13 @@ __device__ __forceinline__ void fin_stage(double *dst, const double *src, int n,
 template <int E>
 __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, FinArgs f) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  if (stopped(a.ctl)) return;  // (uniform: the flag changes only in the last sum / update block below)
+  // A stopped loop: the launch does nothing.  (Not uniform over the launch:
+  // the last sum block sets stop = 2 at the iteration limit, and update
+  // blocks dispatched after that return here without ticking FIN_UT, so no
+  // update block is last and this launch's counters and list counts stay
+  // set.  Every later launch of the loop returns here too, and the next
+  // loop starts with ph_loop_reset, which clears d_fin and the counts.)
+  if (stopped(a.ctl)) return;
   const int b = blockIdx.x, lane = threadIdx.x;
   const int S = a.S, K = a.K, G = f.xa.G;
   int32_t *fin = f.fin;
@@ -3075,6 +3112,7 @@ __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, F
     if (f.prof && lane == 0) atomicMax(&f.prof[17], wall_clock64());
     if (b >= f.tb) return;
     fin_wait(fin + FIN_DONE, f.np, 8, a.err);
+    if (lane == 0) fin_ticket(fin + FIN_TPASS);  // (the resetting block waits for every tail block's)
     const int count = min(fin_load(a.wl2_count), S);
     if (count == 0) return;  // (the usual case: the later blocks see the empty list too)
     if (count > b && (!f.has_md || ws_block_ok(md, a.err))) {
@@ -3197,11 +3235,7 @@ __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, F
       ctl->acc[3] = v[2] > ctl->acc[3] ? v[2] : ctl->acc[3];
       ctl->acc[4] += v[3];
       ctl->acc[5] += v[4];
-      if (f.nu == 0) {  // the launch's counters back to zero
-        for (int q = 0; q < 8; ++q) __hip_atomic_store(fin + FIN_DONE + 16 * q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(fin + FIN_TAIL, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(fin + FIN_SUMT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (f.nu == 0) fin_reset(fin, f.tb, false, a.err);  // the launch's counters back to zero
     }
     return;
   }
@@ -3298,11 +3332,7 @@ __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, F
     ctr[1] = 0;
     ctr[2] = 0;
     ctr[6] = 0;
-    for (int q = 0; q < 8; ++q) __hip_atomic_store(fin + FIN_DONE + 16 * q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(fin + FIN_TAIL, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(fin + FIN_SUMT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(fin + FIN_READY, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(fin + FIN_UT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fin_reset(fin, f.tb, true, a.err);
     if (f.prof) atomicMax(&f.prof[29], wall_clock64());
   }
 }
@@ -3915,6 +3945,8 @@ struct ph_batch {
   double *d_fpart = nullptr;    // finish_kernel's partials
   size_t fpart_cap = 0;
   bool fin_attr = false;
+  size_t fin_occ_lds = 0;        // finish_kernel's LDS at its last occupancy query
+  int fin_resident = 0;          // finish_kernel blocks resident at once (occupancy x CUs)
   bool primed = false;          // the first cached solve's hints were seeded (prime_hints)
   bool fused_ran = false;       // a fused pass ran since ph_loop_reset (ph_loop_fused)
   // active-set cache (polish-size scenarios): [S][CW] doubles + flags
@@ -4291,6 +4323,8 @@ static int super_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_i
   return PH_OK;
 }
 
+static long big_polish_max_contrib();
+
 // Scenarios beyond the mid-size plan (max(n, m) > 3072) take the big path
 // (solve_big.inc): the same analysis, long-line lists instead of tails, the
 // state in HBM workspace slices.
@@ -4307,20 +4341,18 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   // of 10 Iter0 polishes, tools/uc_probe.py; CPU: tools/uc_polish_lab.py), so
   // UC solves by PDHG alone (the per-entry form's size limit below) until
   // the polish does.  A big pattern's analysis first counts the per-entry
-  // form's update contributions without building its lists.
+  // form's update contributions without building its lists, which are built
+  // from the same analysis only when the per-entry polish will run (one
+  // minimum-degree ordering per batch; UC's 58M-entry lists never built).
   const char *se = std::getenv("PHGPU_KKT_SUPER");
   const int super_env = se && *se ? std::atoi(se) : -1;
-  bool lists = !big;
-  if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx, lists))
+  if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx, !big))
     return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
                                (b->sym.error ? b->sym.error : "?"));
   bool use_super = big && super_env == 1;
-  if (big && !use_super) {
-    lists = true;
-    if (!b->sym.analyze(b->n, b->m, row_ptr, col_idx, true))
-      return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
-                                 (b->sym.error ? b->sym.error : "?"));
-  }
+  if (big && !use_super && b->sym.ncontrib <= big_polish_max_contrib() && !b->sym.build_lists())
+    return fail(PH_EINVAL, std::string("ph_batch_create: KKT symbolic analysis refused the pattern: ") +
+                               (b->sym.error ? b->sym.error : "?"));
   const KktSymbolic &y = b->sym;
   auto up2 = [](long v) { return (v + 1) & ~1L; };
   auto up4 = [](long v) { return (v + 3) & ~3L; };
@@ -5918,9 +5950,46 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
   a.prof = nullptr;
   DISPATCH_EXT(64, 1, b->ext, {
     if (fin_lds > 64 * 1024) return fail(PH_EINVAL, "finish_kernel: LDS past 64 KB");
+    const void *kf = (const void *)finish_kernel<E_>;
+    // The in-launch waits assume the hardware dispatches blocks in index
+    // order and that the waiting blocks never hold every slot: the tb tail
+    // blocks wait for all np polish blocks (higher indices), the sum and
+    // update blocks only for lower-index roles.  So at least tb + 1 blocks
+    // must be resident at once (occupancy x CUs, queried per LDS size); with
+    // fewer, tb shrinks.  When several batches share the device (a hub and
+    // its spokes on streams of their own), another stream's kernels can hold
+    // the CUs, so the launch is cooperative (every block placed at once or
+    // refused), np cut so the grid fits the resident capacity.
+    if (b->fin_occ_lds != fin_lds || b->fin_resident <= 0) {
+      int per_cu = 0, cus = 0, dev = 0;
+      HIP_OK(hipGetDevice(&dev));
+      HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, WAVE, fin_lds));
+      b->fin_resident = per_cu * cus;
+      b->fin_occ_lds = fin_lds;
+    }
+    if (b->fin_resident < 2) return fail(PH_EHIP, "finish_kernel: fewer than two resident blocks");
+    if (f.tb + 1 > b->fin_resident) f.tb = b->fin_resident - 1;
+    const bool coop = coop_enabled();
+    if (coop) {
+      const int room = b->fin_resident - f.nsum - f.nu;
+      if (room < 1) return fail(PH_EHIP, "finish_kernel: the cooperative grid does not fit");
+      f.np = std::min(f.np, room);
+      f.tb = std::min(f.tb, f.np);
+    }
     void *args[3] = {&a, &b->md, &f};
-    HIP_OK(hipExtLaunchKernel((const void *)finish_kernel<E_>, dim3(f.np + f.nsum + f.nu), dim3(WAVE), args,
-                              fin_lds, b->stream, tev ? tev[2] : nullptr, tev ? tev[3] : nullptr, 0));
+    const dim3 grid(f.np + f.nsum + f.nu);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_OK(hipStreamIsCapturing(b->stream, &cs));
+    if (coop && cs == hipStreamCaptureStatusNone) {
+      if (tev) HIP_OK(hipEventRecord(tev[2], b->stream));
+      const hipError_t e = hipLaunchCooperativeKernel(kf, grid, dim3(WAVE), args, (unsigned)fin_lds, b->stream);
+      if (e != hipSuccess) return fail(PH_EHIP, std::string("finish_kernel cooperative launch: ") + hipGetErrorString(e));
+      if (tev) HIP_OK(hipEventRecord(tev[3], b->stream));
+    } else {
+      HIP_OK(hipExtLaunchKernel(kf, grid, dim3(WAVE), args, fin_lds, b->stream, tev ? tev[2] : nullptr,
+                                tev ? tev[3] : nullptr, 0));
+    }
   });
   HIP_OK(hipGetLastError());
   return PH_OK;

@@ -11,4 +11,4 @@ grep -E "FAILED|ERROR|passed|failed" $O/pytest_gpu_final.log | tail -20
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_final.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke_final.log; exit 1; }
 tail -3 $O/smoke_final.log
-bash tools/gpu_r04_bench.sh
+bash tools/archive/gpu_r04_bench.sh
