@@ -14,11 +14,15 @@ MI355X form: the bundles of a rank are a second scenario-batched layout
 whose "scenario" is a bundle.  Every bundle has the same shape -- T blocks
 (T = the largest bundle; a shorter bundle's last block is inert: its columns
 fixed at 0, its rows free) of the scenario pattern plus (T - 1) x K
-nonanticipativity rows x_t[k] - x_ref[k] = 0: the reference's star on the
-bundle's first scenario (x_ref = block 0) where slot k is at one node for
-every scenario (two-stage), else a chain x_ref = x_(t-1) (a node's scenarios
-are contiguous), active when both blocks belong to slot k's node and block
-t's nonant is not fixed (nonant_for_fixed_vars=False).  The batched
+nonanticipativity rows x_t[k] - x_ref[k] = 0, x_ref the bundle's first
+scenario at block t's node for slot k (the reference's ref_vars,
+sputils.py:350-364: a star per tree node).  Where slot k is at one node for
+every scenario (two-stage) the reference is block 0 and the row has two
+entries; otherwise the row of block t holds every block 0..t and its values
+(per bundle, like every value of the batch) put -1 on the node's first block
+of that bundle, 0 on the others.  A row is active when block t is real,
+shares the node with an earlier real block and its nonant is not fixed
+(nonant_for_fixed_vars=False).  The batched
 solver runs on that layout unchanged; its PH terms are gathered from the
 scenario arrays with the EF weights p_s / P_b, and its solution is scattered
 back to the scenarios' x (``ph_gather`` in include/phgpu.h).
@@ -92,26 +96,44 @@ class BundleLayout:
         col_idx = [ci + t * n for t in range(T)]
         base = T * nnz
         L = (T - 1) * K
-        row_ptr.append(base + 2 * np.arange(L))
-        # slot k's link rows: a star on block 0 (the reference's ref_vars,
-        # sputils.py:350-363: the bundle's first scenario) when every scenario
-        # has slot k at the same node (two-stage); else a chain t-1 -> t (a
-        # node's scenarios are contiguous)
+        # slot k's link rows: the reference block is block 0 (the bundle's
+        # first scenario) when every scenario has slot k at the same node
+        # (two-stage): entries (0, t); else the node's first block in the
+        # bundle, which differs by bundle: entries (0 .. t), values per bundle
         star = np.all(gid == gid[:, :1], axis=1) if S > 0 else np.ones(K, dtype=bool)
-        link_cols = np.empty((T - 1, K, 2), dtype=np.int64)
+        gext = np.concatenate([gid, np.full((K, 1), -1)], axis=1)
+        fixed = np.concatenate([data.l[nc] == data.u[nc], np.ones((K, 1), dtype=bool)], axis=1)  # [K][S+1]
+        lcols, lvals, lptr = [], [], [0]
+        lrl = np.full((T - 1, K, Sb), -np.inf)
         for t in range(1, T):
-            link_cols[t - 1, :, 0] = np.where(star, 0, t - 1) * n + nc
-            link_cols[t - 1, :, 1] = t * n + nc
-        col_idx.append(link_cols.reshape(-1))
-        row_ptr = np.concatenate(row_ptr + [[base + 2 * L]])
+            gt = gext[:, member[t]]                                   # [K][Sb] block t's node
+            # the node's first real block before t (-1: none)
+            ref = np.full((K, Sb), -1, dtype=np.int64)
+            for tp in range(t - 1, -1, -1):
+                hit = real[tp][None, :] & (gext[:, member[tp]] == gt)
+                ref = np.where(hit, tp, ref)
+            ref = np.where(star[:, None], np.where(real[0][None, :] & (gext[:, member[0]] == gt), 0, -1), ref)
+            on = real[t][None, :] & (ref >= 0) & ~fixed[:, member[t]]
+            lrl[t - 1] = np.where(on, 0.0, -np.inf)
+            for k in range(K):
+                blocks = [0, t] if star[k] else list(range(t + 1))
+                lcols.extend(bk * n + nc[k] for bk in blocks)
+                v = np.zeros((len(blocks), Sb))
+                v[-1] = 1.0
+                for q, bk in enumerate(blocks[:-1]):
+                    v[q] = np.where(ref[k] == bk, -1.0, 0.0)
+                lvals.append(v)
+                lptr.append(lptr[-1] + len(blocks))
+        row_ptr.append(base + np.asarray(lptr[:-1], dtype=np.int64))
+        col_idx.append(np.asarray(lcols, dtype=np.int64))
+        row_ptr = np.concatenate(row_ptr + [[base + lptr[-1]]])
         col_idx = np.concatenate(col_idx)
         mb = T * m + L
         # -- values and data (an extra zero / inert column per array for the pad)
         def take(a, fill):
             ext = np.concatenate([a, np.full((a.shape[0], 1), fill)], axis=1)
             return np.concatenate([ext[:, member[t]] for t in range(T)], axis=0)
-        vals = np.concatenate([take(data.vals, 0.0),
-                               np.tile(np.array([-1.0, 1.0]), L)[:, None].repeat(Sb, axis=1)], axis=0)
+        vals = np.concatenate([take(data.vals, 0.0)] + lvals, axis=0)
         c = np.concatenate([np.concatenate([data.c, np.zeros((n, 1))], axis=1)[:, member[t]] * wt[t][None, :]
                             for t in range(T)], axis=0)
         const = (np.append(data.const, 0.0)[member] * wt).sum(axis=0)
@@ -119,19 +141,11 @@ class BundleLayout:
         ub = take(data.u, 0.0)
         rl = take(data.rl, -np.inf)
         ru = take(data.ru, np.inf)
-        # link rows: active when both blocks are real and share slot k's node,
-        # and the later block's nonant is not fixed in its scenario (the bundle
-        # EF is formed with nonant_for_fixed_vars=False, phbase.py:860-861,
-        # sputils.py:358-360: no row for a fixed Var)
-        gext = np.concatenate([gid, np.full((K, 1), -1)], axis=1)
-        fixed = np.concatenate([data.l[nc] == data.u[nc], np.ones((K, 1), dtype=bool)], axis=1)  # [K][S+1]
-        lrl = np.full((T - 1, K, Sb), -np.inf)
-        for t in range(1, T):
-            mr = np.where(star[:, None], member[0][None, :], member[t - 1][None, :])   # [K][Sb]
-            rr = np.where(star[:, None], real[0][None, :], real[t - 1][None, :])
-            same = real[t][None, :] & rr & (np.take_along_axis(gext, mr, axis=1) == gext[:, member[t]]) & \
-                ~fixed[:, member[t]]
-            lrl[t - 1] = np.where(same, 0.0, -np.inf)
+        # link rows: active when block t is real and shares slot k's node with
+        # an earlier real block, and its nonant is not fixed in its scenario
+        # (the bundle EF is formed with nonant_for_fixed_vars=False,
+        # phbase.py:860-861, sputils.py:358-360: no row for a fixed Var; a
+        # fixed reference still anchors the others)
         lru = np.where(np.isfinite(lrl), 0.0, np.inf)
         rl = np.concatenate([rl, lrl.reshape(L, Sb)], axis=0)
         ru = np.concatenate([ru, lru.reshape(L, Sb)], axis=0)

@@ -12,7 +12,9 @@ import scipy.sparse as sp
 from .solve import _highs_solve
 
 
-def solve_ef(scens):
+def solve_ef(scens, nonant_for_fixed_vars=True):
+    """nonant_for_fixed_vars=False: no row for a fixed (l == u) variable of a
+    later scenario (sputils.py:358-360; the reference's bundles, phbase.py:860-861)."""
     S = len(scens)
     prob = np.array([s.prob if s.prob is not None else 1.0 / S for s in scens])
     sgn = 1.0 if scens[0].sense == "min" else -1.0
@@ -34,6 +36,8 @@ def solve_ef(scens):
                 continue
             r0, ridx = first[nm]
             for a, b in zip(idx, ridx):
+                if not nonant_for_fixed_vars and s.l[a] == s.u[a]:
+                    continue
                 rows.append(((si, a), (r0, b)))
     na = sp.lil_matrix((len(rows), int(offs[-1])))
     for r, ((si, a), (r0, b)) in enumerate(rows):

@@ -520,6 +520,57 @@ def test_bundled_hydro_multistage_matches_oracle():
     assert abs(conv - oc) < 1e-6 * abs(oc)
 
 
+def test_bundle_multistage_fixed_nonant_links_to_node_reference():
+    """A fixed multistage nonant inside a bundle (advisor r5): the reference
+    links every unfixed variable to the node's first scenario in the bundle
+    (sputils.py:350-364, ref_vars) and writes no row for a fixed one
+    (nonant_for_fixed_vars=False), so the later scenarios of the node are
+    tied to the reference scenario, not to the fixed value.  Hydro, the
+    bundle Scen1..Scen4 (ROOT_0's three and one of ROOT_1) with Scen2's
+    stage-2 Vol fixed at 0 (the old chain tied Scen3 to that value: bundle
+    value 108.589 against the reference's 106.375): the bundle's LP equals the
+    oracle's EF with the same fixing."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import hydro
+    from mpisppy_amd.bundles import BundleLayout
+    from mpisppy_amd.batch import BatchData
+    from oracle.ef import solve_ef
+    from oracle.solve import solve_scenario
+    import scipy.sparse as sp
+    names, nodes = hydro.all_names_and_nodes()
+    opts = _opts(branching_factors=[3, 3])
+    ph = PH(dict(opts), names, hydro.scenario_creator, all_nodenames=nodes,
+            scenario_creator_kwargs={"branching_factors": [3, 3]})
+    d0 = ph.batch_data
+    col = list(d0.var_names).index("Vol[2]")
+    assert col in set(d0.nonant_cols.tolist())
+    l, u = d0.l.copy(), d0.u.copy()
+    fix_val = 0.0
+    l[col, 1] = u[col, 1] = fix_val
+    d = BatchData(d0.names, d0.row_ptr, d0.col_idx, d0.vals, d0.c, d0.const, l, u, d0.rl, d0.ru,
+                  d0.nonant_cols, d0.node_infos, d0.sense, prob=d0.prob, var_names=d0.var_names)
+    bl = BundleLayout(d, [[0, 1, 2, 3], [4, 5, 6, 7, 8]], ph.local_prob, ph.gid_host, ["b0", "b1"])
+    bd = bl.data
+    A = sp.csr_matrix((bd.vals[:, 0], bd.col_idx, bd.row_ptr), shape=(bd.m, bd.n))
+    x, y, feas = solve_scenario(bd.c[:, 0], None, A, bd.rl[:, 0], bd.ru[:, 0], bd.l[:, 0], bd.u[:, 0])
+    assert feas
+    val = bl.P[0] * (float(bd.c[:, 0] @ x) + float(bd.const[0]))
+    scens = [om.hydro(nm) for nm in names[:4]]
+    oc = scens[1].var_names.index("Vol[2]")
+    scens[1].l = scens[1].l.copy()
+    scens[1].u = scens[1].u.copy()
+    scens[1].l[oc] = scens[1].u[oc] = fix_val
+    for sc in scens:
+        sc.prob = 1.0 / len(names)
+    ef, xs = solve_ef(scens, nonant_for_fixed_vars=False)
+    assert abs(val - ef) <= 1e-9 * max(1.0, abs(ef)), (val, ef)
+    # Scen3 (block 2) follows Scen1 (the node's reference), not Scen2's fixed value
+    n = d.n
+    assert abs(x[2 * n + col] - x[0 * n + col]) <= 1e-9 * max(1.0, abs(x[col]))
+    assert abs(x[1 * n + col] - fix_val) <= 1e-12
+    assert abs(x[0 * n + col] - fix_val) > 1e-3   # (the fixing is binding: a different EF than the chain's)
+
+
 @pytest.mark.parametrize("by", ["name", "vardata"])
 def test_rho_setter_matches_oracle(by):
     """phbase.py:556-588: rho_setter(scenario) -> [(var, rho)]; the var given
