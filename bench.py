@@ -556,62 +556,76 @@ def sslp_config(args, world, PH, opts):
 
 
 def uc_config(args, world, PH, opts):
-    """BASELINE config 4's model at a reduced scenario count: the LP
-    relaxation of paperruns/larger_uc/ReferenceModel_OK.py on the WECC-240
-    data (examples/uc.py: n = 56,869, m = 69,902, nnz = 240,508 per scenario;
-    Scenario1.. of 1000scenarios_wind, the reference's rho setter), --uc-scens
-    per rank.  The big path with y in the workspace slice, PDHG only (the
-    LDL' factorisation, 58M update contributions, is past the big polish's
-    size limit) on teams of blocks (a short list shares the resident grid).
-    Iter0 (LPs to 1e-9), then --uc-steps PH iterations (prox-QPs, host
-    loop).  1,000 scenarios are out of reach of a bench run on this path: at
-    ~400k PDHG steps per LP one block per scenario streams ~10 MB per step."""
+    """BASELINE config 4's model and cylinder structure at a reduced
+    scenario count: the LP relaxation of paperruns/larger_uc/ReferenceModel_OK.py
+    on the WECC-240 data (examples/uc.py: n = 56,869, m = 69,902,
+    nnz = 240,508 per scenario; Scenario1.. of 1000scenarios_wind, the
+    reference's rho setter), --uc-scens per rank, run as
+    examples/uc/uc_cylinders.py runs it: a PH hub (:86) with a Lagrangian
+    outer-bound spoke (:138-159) and an xhat shuffle inner-bound spoke through
+    spin_the_wheel (:167), the spokes asynchronous on streams of their own,
+    1 + --uc-steps hub iterations.  The big path with y in the workspace
+    slice, PDHG only (the LDL' factorisation, 58M update contributions, is
+    past the big polish's size limit; DESIGN 4.11 records the interior-point
+    attempt) on teams of blocks.  ms per PH iteration = the hub's solve_loop
+    wall time per iteration (spokes overlapping); 1,000 scenarios are out of
+    reach on this path (~400k PDHG steps per LP at ~10 MB per step)."""
     from mpisppy_amd.examples import uc
+    from mpisppy_amd.phbase import PHBase
+    from mpisppy_amd.cylinders.hub import PHHub
+    from mpisppy_amd.cylinders.lagrangian_bounder import LagrangianOuterBound
+    from mpisppy_amd.cylinders.xhatshufflelooper_bounder import XhatShuffleInnerBound
+    from mpisppy_amd.utils.sputils import spin_the_wheel
     S = args.uc_scens * world
     o = dict(opts)
     o["iter0_solver_options"] = {"pdhg_max_iters": 1000000}
     o["iterk_solver_options"] = {"pdhg_max_iters": 400000}
     o["device_loop"] = False
-    ph = PH(o, uc.all_scenario_names(S), uc.scenario_creator, rho_setter=uc.scenario_rhos)
-    ph.PH_Prep()
-    ph.subproblem_creation()
-    ph._create_solvers()
-    b = ph.batch
-    torch.cuda.synchronize()
-    _progress("UC Iter0")
-    t0 = time.perf_counter()
-    tb = ph.Iter0()
-    torch.cuda.synchronize()
-    t_iter0 = time.perf_counter() - t0
-    it0 = b.iters.cpu().numpy()
-    nonopt0 = int((b.status != 0).sum().item())
+    iters = 1 + args.uc_steps
+    base = dict(scenario_creator=uc.scenario_creator, all_scenario_names=uc.all_scenario_names(S),
+                rho_setter=uc.scenario_rhos)
+    hub_dict = {"hub_class": PHHub, "hub_kwargs": {"options": {"rel_gap": None}, "sync_every": 1,
+                                                   "async_spokes": True},
+                "opt_class": PH, "opt_kwargs": dict(PHoptions=dict(o, PHIterLimit=iters, convthresh=-1.0), **base)}
+    spokes = [{"spoke_class": LagrangianOuterBound, "opt_class": PHBase,
+               "opt_kwargs": dict(PHoptions=dict(o, PHIterLimit=iters), **base)},
+              {"spoke_class": XhatShuffleInnerBound, "opt_class": PHBase,
+               "opt_kwargs": dict(PHoptions=dict(o, PHIterLimit=iters), **base)}]
+    _progress("UC hub + Lagrangian + xhat spokes")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    steps = []
-    for _ in range(args.uc_steps):
-        ph.Compute_Xbar()
-        ph.Update_W(False)
-        ph.solve_loop(solver_options=ph.current_solver_options)
-        steps.append(float(b.iters.float().mean().item()))
+    with contextlib.redirect_stdout(sys.stderr):  # (the hub's trace table: stdout holds the one JSON line)
+        hub, _ = spin_the_wheel(hub_dict, spokes)
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    d = torch.tensor([dt], dtype=torch.float64, device=_red_dev())
+    wall = time.perf_counter() - t0
+    ph = hub.opt
+    b = ph.batch
+    log = list(ph.solve_log)   # (solves, seconds) per solve_loop: Iter0 first
+    t_iter0 = log[0][1] if log else float("nan")
+    tk = [t for _, t in log[1:1 + args.uc_steps]]
+    d = torch.tensor([sum(tk)], dtype=torch.float64, device=_red_dev())
     if world > 1:
         dist.all_reduce(d, op=dist.ReduceOp.MAX)
-    dt = float(d.item())
+    lag = hub.spokes[0]
     return {"workload": f"UC LP relaxation (ReferenceModel_OK.py, WECC-240), {S} scenarios "
                         f"({args.uc_scens} per GPU), n={b.n}, m={b.m}, nnz={b.nnz} per scenario, "
-                        "reference rho setter",
-            "iter0_s": round(t_iter0, 2), "iter0_not_optimal": nonopt0, "trivial_bound": tb,
-            "iter0_pdhg_steps_mean": round(float(it0.mean()), 1), "iter0_pdhg_steps_max": int(it0.max()),
+                        "reference rho setter; PH hub + Lagrangian + xhat shuffle spokes (uc_cylinders.py)",
+            "iter0_s": round(t_iter0, 2), "trivial_bound": ph.trivial_bound,
             "ph_iterations": args.uc_steps,
-            "ms_per_ph_iteration": round(dt / max(args.uc_steps, 1) * 1000.0, 1),
-            "pdhg_steps_per_prox_qp": [round(v, 1) for v in steps],
+            "ms_per_ph_iteration": round(float(d.item()) / max(len(tk), 1) * 1000.0, 1),
+            "published_ms_per_ph_iteration": 910.0,
+            "published_note": "examples/uc/quartz/10scen_nofw.baseline.out:8,107: iteration 1 at 29.25 s, "
+                              "100 at 119.22 s -- the MIP, 10 scenarios on 30 ranks (2 nodes), gurobi",
+            "lagrangian_bound": lag.bound, "best_outer_bound": hub.BestOuterBound,
+            "best_inner_bound": hub.BestInnerBound, "rel_gap": hub.compute_gap(True),
             "not_optimal_after": int((b.status != 0).sum().item()),
+            "wall_s": round(wall, 2),
             "parity": "unpinned (no reference file holds UC LP values); the oracle restatement matches "
-                      "the Iter0 bounds to 2e-9 (tests/test_gpu_parity.py::test_uc_lp_relaxation_matches_oracle)"}
+                      "the Iter0 bounds to 2e-9 (tests/test_gpu_parity.py::test_uc_lp_relaxation_matches_oracle) "
+                      "and the cylinders' bounds bracket the oracle EF at 2 scenarios "
+                      "(test_uc_hub_lagrangian_xhat_bracket_the_extensive_form)"}
 
 
 def _spawn_ranks(n, cpu):

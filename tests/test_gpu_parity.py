@@ -988,6 +988,58 @@ def test_async_spokes_with_teams_match_sync():
     assert min(a[1], s[1]) >= s[0] * (1 - 1e-9) if s[0] > 0 else min(a[1], s[1]) >= s[0] * (1 + 1e-9)
 
 
+def test_uc_hub_lagrangian_xhat_bracket_the_extensive_form():
+    """BASELINE config 4 as the reference configures it, at 2 scenarios:
+    examples/uc/uc_cylinders.py:86 (PH hub), :138-159 (Lagrangian spoke),
+    :167 (spin_the_wheel), plus the xhat shuffle inner-bound spoke, with the
+    reference's rho setter (uc_funcs.py:94-112), async spokes on streams of
+    their own.  The model is the LP relaxation of
+    paperruns/larger_uc/ReferenceModel_OK.py (examples/uc.py).  PARITY
+    UNPINNED (no reference file holds a UC LP value): the bracket is checked
+    against the oracle's extensive form of Scenario1..2
+    (tests/golden/uc_lp_values.json "ef", HiGHS simplex on oracle/models.uc):
+    the hub's best outer bound (the trivial bound or the Lagrangian spoke's
+    safe bound) <= EF <= its best inner bound (an xhat the spoke evaluated),
+    and the Lagrangian spoke did report a finite bound."""
+    import json
+    import math
+    import os
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.phbase import PHBase
+    from mpisppy_amd.cylinders.hub import PHHub
+    from mpisppy_amd.cylinders.lagrangian_bounder import LagrangianOuterBound
+    from mpisppy_amd.cylinders.xhatshufflelooper_bounder import XhatShuffleInnerBound
+    from mpisppy_amd.utils.sputils import spin_the_wheel
+    from mpisppy_amd.examples import uc
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "uc_lp_values.json")))
+    ef = gold["ef"]["2"]
+    names = uc.all_scenario_names(2)
+
+    def uc_opts(**kw):
+        o = _opts(**kw)
+        o["iter0_solver_options"] = {"pdhg_max_iters": 400000}
+        o["iterk_solver_options"] = {"pdhg_max_iters": 200000}
+        o["device_loop"] = False
+        return o
+    base = dict(scenario_creator=uc.scenario_creator, all_scenario_names=names, rho_setter=uc.scenario_rhos)
+    hub_dict = {"hub_class": PHHub, "hub_kwargs": {"options": {"rel_gap": None}, "sync_every": 1,
+                                                   "async_spokes": True},
+                "opt_class": PH,
+                "opt_kwargs": dict(PHoptions=uc_opts(PHIterLimit=3, convthresh=-1.0), **base)}
+    spokes = [{"spoke_class": LagrangianOuterBound, "opt_class": PHBase,
+               "opt_kwargs": dict(PHoptions=uc_opts(PHIterLimit=3), **base)},
+              {"spoke_class": XhatShuffleInnerBound, "opt_class": PHBase,
+               "opt_kwargs": dict(PHoptions=uc_opts(PHIterLimit=3), **base)}]
+    hub, _ = spin_the_wheel(hub_dict, spokes)
+    assert hub.opt._PHIter == 3
+    lag = hub.spokes[0]
+    assert lag.bound is not None and math.isfinite(lag.bound), lag.bound
+    assert lag.bound <= ef * (1 + 1e-9), (lag.bound, ef)
+    assert hub.BestOuterBound <= ef * (1 + 1e-9), (hub.BestOuterBound, ef)
+    assert math.isfinite(hub.BestInnerBound) and hub.BestInnerBound >= ef * (1 - 1e-9), (hub.BestInnerBound, ef)
+    assert hub.BestOuterBound >= 0.99 * ef   # (a bound, not a vacuous one)
+
+
 def test_wxbar_files_from_the_hip_path_match_oracle_and_resume(tmp_path):
     """SURVEY 8 f-3 on the HIP path (utils/wxbarutils.py:40-79, 264-284 via
     the WXBarWriter / WXBarReader extensions): a GPU PH on farmer S=12 writes
