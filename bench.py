@@ -580,6 +580,7 @@ def uc_config(args, world, PH, opts):
     o = dict(opts)
     o["iter0_solver_options"] = {"pdhg_max_iters": 1000000}
     o["iterk_solver_options"] = {"pdhg_max_iters": 400000}
+    o["xhat_max_iters"] = 400000
     o["device_loop"] = False
     iters = 1 + args.uc_steps
     base = dict(scenario_creator=uc.scenario_creator, all_scenario_names=uc.all_scenario_names(S),

@@ -133,6 +133,7 @@ class PHBase(SPBase):
         self.conv_w = torch.as_tensor(wconv, **f64)
         self.conv_hist = None
         self._loop_graphs = {}
+        self._graphs_failed = False
         self.scenario_feasible = np.ones(S, dtype=bool)
         self._all_feasible = True
 
@@ -450,7 +451,9 @@ class PHBase(SPBase):
         library's kernels run there; under RCCL the collective is queued on
         torch's current stream)."""
         ts = getattr(self.batch, "torch_stream", None)
-        if ts is None or not t.is_cuda:
+        if ts is None or not t.is_cuda or torch.cuda.is_current_stream_capturing():
+            # (under graph capture: the capture stream, which the batch's
+            # launches also use, so the collective is a node of the graph)
             return self.comm.allreduce_(t)
         with torch.cuda.stream(ts):
             return self.comm.allreduce_(t)
@@ -720,7 +723,7 @@ class PHBase(SPBase):
         (pre-weighted) convergence partial; the previous pass's convergence
         test runs inside the call and, if it stops, the host restores the
         x/y saved before that pass's solve (run_device_loop)."""
-        if self.comm.size > 1:
+        if self._pass_collective():
             self._allreduce(self.xpass)
         self.batch.loop_pass()
 
@@ -729,7 +732,7 @@ class PHBase(SPBase):
         persistent launch that keeps the scenarios' data in LDS across the
         passes when the batch qualifies, else the per-pass kernels); several
         ranks: one ph_loop_pass per pass after its allreduce."""
-        if self.comm.size == 1:
+        if not self._pass_collective():
             self.batch.loop_run(chunk)
         else:
             for _ in range(chunk):
@@ -739,7 +742,7 @@ class PHBase(SPBase):
         """ph_loop_bind_pass: the device loop's per-pass arguments, once."""
         b = self.batch
         saves = None
-        if self.comm.size > 1:
+        if self._pass_collective():
             if self._x_save is None:
                 self._x_save = torch.empty_like(b.x)
                 self._y_save = torch.empty_like(b.y)
@@ -748,7 +751,7 @@ class PHBase(SPBase):
             saves = (self._x_save, self._y_save, self._st_save, self._db_save)
         b.loop_bind_pass(self.xsums, self.G, self.gid, self.rho, self.w_coeff, self.xbar,
                          self.xsqbar, self.W, self.absdiff, self.conv_w, self.conv_hist,
-                         self.conv_part if self.comm.size > 1 else None, saves,
+                         self.conv_part if self._pass_collective() else None, saves,
                          self.w_on, self.prox_on, **kw)
 
     def run_device_loop(self, start_iter, iter_limit, convthresh, chunk=None):
@@ -779,7 +782,8 @@ class PHBase(SPBase):
             graph = self._loop_graphs.get(key)
             if graph is None:
                 graph = self._capture_chunk(kw, chunk)
-                self._loop_graphs[key] = graph
+                if graph is not None:
+                    self._loop_graphs[key] = graph
         try:
             while True:
                 t0 = time.perf_counter()
@@ -798,7 +802,7 @@ class PHBase(SPBase):
                                            it_max, npol - prev[1]))
                 if stop:
                     break
-            if self.comm.size > 1:
+            if self._pass_collective():
                 # the last pass's conv partial (limit reached), then the
                 # reference's state at a convergence break: x/y of before the
                 # solve that the lagged test showed should not have run
@@ -825,10 +829,18 @@ class PHBase(SPBase):
         self._set_feasibility(nonopt, True, kw["max_iters"])
         return stop, it
 
+    def _pass_collective(self):
+        """The several-ranks form of a device-loop pass (one collective of the
+        node sums + the lagged convergence partial before each ph_loop_pass):
+        several ranks, or the option device_loop_collective (one rank running
+        that form, for tests of its capture)."""
+        return self.comm.size > 1 or bool(self.PHoptions.get("device_loop_collective", False))
+
     def _graph_ok(self):
         """Replay chunks of the device loop as one HIP graph (option
-        device_loop_graphs, default off): a single GPU rank (collectives stay
-        eager) on a CUDA device.  With one ph_loop_pass call per iteration
+        device_loop_graphs: True / False / "auto", the default: graphs only
+        for several ranks on RCCL, whose collectives are captured with the
+        passes).  One rank:  With one ph_loop_pass call per iteration
         the eager loop issues in ~21 us against ~60 us of GPU work per F2
         iteration, and measured faster than the graph replay
         (profiles/r03: 0.0601 / 0.0612 against 0.0629 / 0.0658 ms per step).
@@ -838,8 +850,19 @@ class PHBase(SPBase):
         device-side checks now turn a recurrence into PH_EDEV),
         so keep the option off outside tests and measurements."""
         b = self.batch
-        return (self.PHoptions.get("device_loop_graphs", False) and self.comm.size == 1
-                and self.device.type == "cuda" and hasattr(b, "set_stream"))
+        if self._graphs_failed or self.device.type != "cuda" or not hasattr(b, "set_stream"):
+            return False
+        opt = self.PHoptions.get("device_loop_graphs", "auto")
+        coll = self._pass_collective()
+        if coll and self.comm.size > 1 and self.comm.backend != "nccl":
+            return False   # (gloo stages collectives through the host: not capturable)
+        if opt == "auto":
+            # several ranks on RCCL: the pass is a collective + one library
+            # call, each a host round trip of ~10-20 us against ~50 us of GPU
+            # work at F2, so the chunk is replayed as one graph with the
+            # collectives captured on the batch's stream
+            return coll and self.comm.size > 1
+        return bool(opt)
 
     def _capture_chunk(self, kw, chunk):
         """Capture `chunk` device iterations (the library's launches moved to
@@ -847,13 +870,23 @@ class PHBase(SPBase):
         b = self.batch
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g):
-            b.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
-            try:
-                for _ in range(chunk):  # (the per-pass kernels: captured as a graph)
-                    self._device_iteration(kw)
-            finally:
-                b.set_stream(b.stream_handle)
+        try:
+            with torch.cuda.graph(g):
+                b.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+                try:
+                    for _ in range(chunk):  # (the per-pass kernels and collectives: one graph)
+                        self._device_iteration(kw)
+                finally:
+                    b.set_stream(b.stream_handle)
+        except RuntimeError as e:
+            # (a capture the runtime refuses -- e.g. a collective library
+            # without stream capture -- leaves the eager passes, which are
+            # the same computation; nothing of the failed capture ran)
+            self._graphs_failed = True
+            if self.cylinder_rank == 0:
+                print(f"device loop: graph capture failed ({e}); eager passes")
+            torch.cuda.synchronize(self.device)
+            return None
         return g
 
     def iterk_loop(self):

@@ -347,6 +347,52 @@ def test_farmer_ragged_sizes_and_reference_rank_count(S, R):
         assert abs(conv - oc) / abs(oc) < 1e-3
 
 
+def test_collective_pass_captured_as_graph_matches_single_rank():
+    """The several-ranks form of the device-loop pass (an allreduce of the
+    node sums and the lagged convergence partial before each ph_loop_pass,
+    phbase._device_iteration) replayed as a HIP graph with the RCCL
+    collective captured on the batch's stream (device_loop_graphs "auto" on
+    several ranks).  One rank in an RCCL process group
+    (option device_loop_collective: the several-ranks form at size 1, where
+    the allreduce is an identity), eager and captured, against the plain
+    single-rank loop: the same iteration count at a convergence break and
+    the same trajectory.  The capture must not fall back to eager."""
+    import socket
+    import torch.distributed as dist
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    names = [f"scen{i}" for i in range(300)]
+
+    def run(**mode):
+        opts = _opts(PHIterLimit=200, defaultPHrho=1.0, convthresh=2e-4, device_loop_chunk=8, **mode)
+        ph = PH(dict(opts), names, farmer.scenario_creator)
+        conv, eobj, tb = ph.ph_main()
+        return ph, (ph._PHIter, conv, eobj, ph.xbar.cpu().numpy().copy(), ph.W.cpu().numpy().copy())
+    _, ref = run(device_loop_graphs=False)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        out = []
+        for graphs in (False, True):
+            ph, r = run(device_loop_collective=True, device_loop_graphs=graphs)
+            assert ph.comm.backend == "nccl" and ph._pass_collective()
+            if graphs:
+                assert not ph._graphs_failed and len(ph._loop_graphs) > 0
+            out.append(r)
+    finally:
+        dist.destroy_process_group()
+    it0, c0, e0, x0, w0 = ref
+    assert it0 < 200
+    for it, c, e, x, w in out:
+        assert it == it0, (it, it0)
+        assert abs(c - c0) <= 1e-9 * abs(c0)
+        assert abs(e - e0) <= 1e-10 * abs(e0)
+        assert _rel(x, x0) < 1e-10
+        assert _rel(w, w0) < 5e-8
+
+
 def test_host_loop_device_loop_and_graphs_agree():
     """The three ways of running iterk_loop (host loop with one solve_loop per
     iteration, device loop with eager launches, device loop replayed as HIP
@@ -1019,6 +1065,7 @@ def test_uc_hub_lagrangian_xhat_bracket_the_extensive_form():
         o = _opts(**kw)
         o["iter0_solver_options"] = {"pdhg_max_iters": 400000}
         o["iterk_solver_options"] = {"pdhg_max_iters": 200000}
+        o["xhat_max_iters"] = 400000   # (a UC LP with its UnitOn fixed: past the 50k default)
         o["device_loop"] = False
         return o
     base = dict(scenario_creator=uc.scenario_creator, all_scenario_names=names, rho_setter=uc.scenario_rhos)
