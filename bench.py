@@ -280,6 +280,31 @@ def _progress(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+class _heartbeat:
+    """A progress line on stderr every `every` s while a long phase runs (a
+    GPU call that writes nothing for 3 minutes is taken to be hung)."""
+
+    def __init__(self, what, every=45.0):
+        import threading
+        self.what, self.every = what, every
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self._stop.wait(self.every):
+            print(f"[bench] {self.what}: {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *a):
+        self._stop.set()
+        self._t.join()
+        return False
+
+
 def _red_dev():
     """Device of the timing max-reductions: the GPU under RCCL, host under gloo."""
     if dist.is_initialized() and dist.get_backend() == "gloo":
@@ -477,7 +502,8 @@ def big_config(args, world, farmer, PH, opts):
     if world > 1:
         dist.all_reduce(d, op=dist.ReduceOp.MAX)
     dt = float(d.item())
-    bracket = f4_bracket(ph, 1 + args.hbm_steps, tb, -1.334838651e8 if (S == 1000 and c == 1000) else None)
+    bracket = (f4_bracket(ph, 1 + args.hbm_steps, tb, -1.334838651e8 if (S == 1000 and c == 1000) else None)
+               if args.f4_bracket else None)
     n, m, nnz = b.n, b.m, b.nnz
     bit = 8 * (2 * nnz + 7 * n + 5 * m)
     steps = st[4]
@@ -562,8 +588,9 @@ def uc_config(args, world, PH, opts):
     nnz = 240,508 per scenario; Scenario1.. of 1000scenarios_wind, the
     reference's rho setter), --uc-scens per rank, run as
     examples/uc/uc_cylinders.py runs it: a PH hub (:86) with a Lagrangian
-    outer-bound spoke (:138-159) and an xhat shuffle inner-bound spoke through
-    spin_the_wheel (:167), the spokes asynchronous on streams of their own,
+    outer-bound spoke (:138-159) through spin_the_wheel (:167), the spoke
+    asynchronous on a stream of its own (an xhat spoke's fixed-UnitOn LPs
+    take past 400k PDHG steps each on this path: not in the line),
     1 + --uc-steps hub iterations.  The big path with y in the workspace
     slice, PDHG only (the LDL' factorisation, 58M update contributions, is
     past the big polish's size limit; DESIGN 4.11 records the interior-point
@@ -574,7 +601,6 @@ def uc_config(args, world, PH, opts):
     from mpisppy_amd.phbase import PHBase
     from mpisppy_amd.cylinders.hub import PHHub
     from mpisppy_amd.cylinders.lagrangian_bounder import LagrangianOuterBound
-    from mpisppy_amd.cylinders.xhatshufflelooper_bounder import XhatShuffleInnerBound
     from mpisppy_amd.utils.sputils import spin_the_wheel
     S = args.uc_scens * world
     o = dict(opts)
@@ -589,15 +615,13 @@ def uc_config(args, world, PH, opts):
                                                    "async_spokes": True},
                 "opt_class": PH, "opt_kwargs": dict(PHoptions=dict(o, PHIterLimit=iters, convthresh=-1.0), **base)}
     spokes = [{"spoke_class": LagrangianOuterBound, "opt_class": PHBase,
-               "opt_kwargs": dict(PHoptions=dict(o, PHIterLimit=iters), **base)},
-              {"spoke_class": XhatShuffleInnerBound, "opt_class": PHBase,
                "opt_kwargs": dict(PHoptions=dict(o, PHIterLimit=iters), **base)}]
-    _progress("UC hub + Lagrangian + xhat spokes")
+    _progress("UC hub + Lagrangian spoke")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with contextlib.redirect_stdout(sys.stderr):  # (the hub's trace table: stdout holds the one JSON line)
+    with contextlib.redirect_stdout(sys.stderr), _heartbeat("UC cylinders"):  # (stdout: the one JSON line)
         hub, _ = spin_the_wheel(hub_dict, spokes)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -612,7 +636,7 @@ def uc_config(args, world, PH, opts):
     lag = hub.spokes[0]
     return {"workload": f"UC LP relaxation (ReferenceModel_OK.py, WECC-240), {S} scenarios "
                         f"({args.uc_scens} per GPU), n={b.n}, m={b.m}, nnz={b.nnz} per scenario, "
-                        "reference rho setter; PH hub + Lagrangian + xhat shuffle spokes (uc_cylinders.py)",
+                        "reference rho setter; PH hub + Lagrangian spoke (uc_cylinders.py)",
             "iter0_s": round(t_iter0, 2), "trivial_bound": ph.trivial_bound,
             "ph_iterations": args.uc_steps,
             "ms_per_ph_iteration": round(float(d.item()) / max(len(tk), 1) * 1000.0, 1),
@@ -620,13 +644,12 @@ def uc_config(args, world, PH, opts):
             "published_note": "examples/uc/quartz/10scen_nofw.baseline.out:8,107: iteration 1 at 29.25 s, "
                               "100 at 119.22 s -- the MIP, 10 scenarios on 30 ranks (2 nodes), gurobi",
             "lagrangian_bound": lag.bound, "best_outer_bound": hub.BestOuterBound,
-            "best_inner_bound": hub.BestInnerBound, "rel_gap": hub.compute_gap(True),
             "not_optimal_after": int((b.status != 0).sum().item()),
             "wall_s": round(wall, 2),
             "parity": "unpinned (no reference file holds UC LP values); the oracle restatement matches "
                       "the Iter0 bounds to 2e-9 (tests/test_gpu_parity.py::test_uc_lp_relaxation_matches_oracle) "
-                      "and the cylinders' bounds bracket the oracle EF at 2 scenarios "
-                      "(test_uc_hub_lagrangian_xhat_bracket_the_extensive_form)"}
+                      "and the hub's bounds bracket the oracle EF at 2 scenarios "
+                      "(test_uc_hub_lagrangian_bracket_the_extensive_form)"}
 
 
 def _spawn_ranks(n, cpu):
@@ -721,6 +744,8 @@ def _parser():
     ap.add_argument("--f4-scens", type=int, default=1000,
                     help="scenarios per rank of the F4 companion config (big path); 0 = skip")
     ap.add_argument("--f4-crops", type=int, default=1000)
+    ap.add_argument("--f4-bracket", type=int, default=1,
+                    help="F4: the EF bracket after the window (0: off, e.g. for a PMC window of the PH solves)")
     ap.add_argument("--sslp-scens", type=int, default=10000,
                     help="scenarios per rank of the sslp companion config (BASELINE config 5); 0 = skip")
     ap.add_argument("--uc-scens", type=int, default=4,

@@ -5037,7 +5037,17 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     b->ev_used += 4;
     HIP_OK(hipEventRecord(tev[0], b->stream));
   }
-  const bool tr = !b->big && b->d_xt;  // the scenario-slowest copies (mid-size path)
+  // the scenario-slowest copies of x, y and the PH terms: a block per
+  // scenario reads its lines as contiguous runs instead of one cache line per
+  // element (mid-size path, and the big path: its polish's sweeps read the PH
+  // terms of every nonant column, 3 lines each per column and sweep at
+  // stride S -- F4's big_polish_kernel moved 23 GB per launch that way)
+  // (PHGPU_BIG_TR=0: measurement hook, the big path on the [line][S] arrays)
+  static const bool big_tr = [] {
+    const char *e = std::getenv("PHGPU_BIG_TR");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const bool tr = b->d_xt != nullptr && (!b->big || big_tr);
   auto tgrid = [&](int R) { return dim3((b->S + TT - 1) / TT, (R + TT - 1) / TT); };
   if (tr) {
     hipLaunchKernelGGL(t_gather_kernel, tgrid(b->n), dim3(256), 0, b->stream, a.x, b->n, b->S, b->d_xt, b->n, 0,

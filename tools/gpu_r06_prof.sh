@@ -39,7 +39,7 @@ NOCPU="--tol-run 0 --no-cpu-baseline"
 on f3 && { prof f3 5 farmer10k_c100 $NOCPU --only f3 --hbm-steps 5 --warmup 5 || exit 1; }
 on sslp && { prof sslp 5 sslp10k $NOCPU --only sslp --hbm-steps 5 --warmup 5 || exit 1; }
 if on f4; then
-  prof f4 5 farmer1k_c1000 $NOCPU --only f4 --hbm-steps 5 || exit 1
+  prof f4 5 farmer1k_c1000 $NOCPU --only f4 --hbm-steps 5 --f4-bracket 0 || exit 1
   python3 tools/pmc_summary.py $O/f4_fetch $O/f4_write $O/f4_stats $O/pmc_summary_f4_iter0.json farmer1k_c1000 first > /dev/null || { echo "pmc f4 iter0 summary failed"; exit 1; }
   cp $O/pmc_summary_f4_iter0.json profiles/$TAG/
 fi
