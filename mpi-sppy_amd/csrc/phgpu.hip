@@ -4901,15 +4901,19 @@ static int big_init(ph_batch *b) {
   } else {
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, big_kernel<false>, BIG_BLOCK, b->big_lds_bytes));
   }
-  HIP_OK(hipFuncSetAttribute((const void *)big_polish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)b->big_plds_bytes));
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, big_polish_kernel, BIG_PBLOCK,
-                                                      b->big_plds_bytes));
+  // (the supernodal instance only when the batch factors supernodally)
+  const void *polish_fn = b->bg.sd_on ? (const void *)big_polish_kernel<true> : (const void *)big_polish_kernel<false>;
+  HIP_OK(hipFuncSetAttribute(polish_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b->big_plds_bytes));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_p, polish_fn, BIG_PBLOCK, b->big_plds_bytes));
   if (per_cu < 1 || per_cu_p < 1) return fail(PH_EINVAL, "ph_batch_bind: the big-path kernels cannot be resident");
   int grid = std::min(b->S, std::min(per_cu, per_cu_p) * std::max(1, cus));
   if (const int cap = mid_grid_cap()) grid = std::min(grid, cap);
   b->big_grid = grid;
   b->bg.ws_blocks = grid;
+  {  // (PHGPU_BIG_QP_PDAS=1: a warm prox-QP polish classifies by the PDAS rule; A/B hook)
+    const char *e = std::getenv("PHGPU_BIG_QP_PDAS");
+    b->bg.qp_pdas = e && std::atoi(e) != 0 ? 1 : 0;
+  }
   int rc = 0;
   if ((rc = dalloc(&b->d_bws, (size_t)grid * b->bg.ws_stride)) ||
       (rc = dalloc(&b->d_vals_t, (size_t)b->S * b->nnz)) || (rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) ||
@@ -5109,8 +5113,12 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
     const MidPhase ph{in, cin, out, cout, q, 0.0, 0, mode, 0, 0};
     if (int rc = phase_event(b, 1)) return rc;
     if (b->big) {
-      hipLaunchKernelGGL(big_polish_kernel, dim3(b->big_grid), dim3(BIG_PBLOCK), b->big_plds_bytes, b->stream,
-                         a, b->md, b->bg, ph);
+      if (b->bg.sd_on)
+        hipLaunchKernelGGL(big_polish_kernel<true>, dim3(b->big_grid), dim3(BIG_PBLOCK), b->big_plds_bytes,
+                           b->stream, a, b->md, b->bg, ph);
+      else
+        hipLaunchKernelGGL(big_polish_kernel<false>, dim3(b->big_grid), dim3(BIG_PBLOCK), b->big_plds_bytes,
+                           b->stream, a, b->md, b->bg, ph);
       HIP_OK(hipGetLastError());
       return phase_event(b, -1);
     }

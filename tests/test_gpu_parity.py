@@ -1086,12 +1086,17 @@ def test_uc_hub_lagrangian_bracket_the_extensive_form():
     # the implementable side: UnitOn at the hub's x-bar, recourse by the oracle
     d = ph.batch_data
     xb = ph.xbar.view(ph.K, ph.S_loc)[:, 0].cpu().numpy()
+    # (UnitOn within 1e-6 of a bound to the bound: the LP relaxation pins many
+    # of them exactly -- initial up / down times -- and a value 1e-10 inside
+    # makes the fixed LP infeasible; any point of [0, 1] is a first stage)
+    xb = np.where(xb < 1e-6, 0.0, np.where(xb > 1.0 - 1e-6, 1.0, xb))
     inner = 0.0
     for s in range(d.S):
         A = sp.csr_matrix((d.vals[:, s], d.col_idx, d.row_ptr), shape=(d.m, d.n))
         l, u = d.l[:, s].copy(), d.u[:, s].copy()
         l[d.nonant_cols] = u[d.nonant_cols] = xb
         st, x, _, _ = _highs_solve(d.c[:, s], None, A, d.rl[:, s], d.ru[:, s], l, u, time_limit=300)
+        assert "Optimal" in str(st), st
         inner += 0.5 * (float(d.c[:, s] @ x) + float(d.const[s]))
     assert inner >= ef * (1 - 1e-9), (inner, ef)
 
