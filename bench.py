@@ -648,7 +648,7 @@ def uc_config(args, world, PH, opts):
             "wall_s": round(wall, 2),
             "parity": "unpinned (no reference file holds UC LP values); the oracle restatement matches "
                       "the Iter0 bounds to 2e-9 (tests/test_gpu_parity.py::test_uc_lp_relaxation_matches_oracle) "
-                      "and the hub's bounds bracket the oracle EF at 2 scenarios "
+                      "and the hub's outer bounds lie within 1 % below the oracle EF at 2 scenarios "
                       "(test_uc_hub_lagrangian_bracket_the_extensive_form)"}
 
 
