@@ -627,9 +627,9 @@ def uc_config(args, world, PH, opts):
     wall = time.perf_counter() - t0
     ph = hub.opt
     b = ph.batch
-    log = list(ph.solve_log)   # (solves, seconds) per solve_loop: Iter0 first
+    log = list(ph.solve_log)   # (solves, seconds, ...) per solve_loop: Iter0 first
     t_iter0 = log[0][1] if log else float("nan")
-    tk = [t for _, t in log[1:1 + args.uc_steps]]
+    tk = [e[1] for e in log[1:1 + args.uc_steps]]
     d = torch.tensor([sum(tk)], dtype=torch.float64, device=_red_dev())
     if world > 1:
         dist.all_reduce(d, op=dist.ReduceOp.MAX)
@@ -748,7 +748,7 @@ def _parser():
                     help="F4: the EF bracket after the window (0: off, e.g. for a PMC window of the PH solves)")
     ap.add_argument("--sslp-scens", type=int, default=10000,
                     help="scenarios per rank of the sslp companion config (BASELINE config 5); 0 = skip")
-    ap.add_argument("--uc-scens", type=int, default=4,
+    ap.add_argument("--uc-scens", type=int, default=2,
                     help="scenarios per rank of the UC companion config (BASELINE config 4's model); 0 = skip")
     ap.add_argument("--uc-steps", type=int, default=1, help="PH iterations of the UC companion")
     ap.add_argument("--only", choices=["f3", "f4", "sslp", "uc"], default=None,
