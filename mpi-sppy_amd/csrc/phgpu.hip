@@ -4003,6 +4003,8 @@ struct ph_batch {
   int mid_grid = 0, mid_pgrid = 0;  // resident blocks of the PDHG / polish phase kernels
   int32_t *d_mlist = nullptr;  // [5][S] phase work lists
   int32_t *d_mctr = nullptr;   // [16] list counts (0..4) and queue counters (8..13)
+  int8_t *d_aset = nullptr;    // [S][n + m] the mid-size polish's accepted sets (MidArgs::aset)
+  int32_t *d_aset_ok = nullptr;  // [S]
   int32_t *d_err = nullptr;    // [4] device-side invariant checks (dev_fail)
   ph_loop_pass_args pass{};    // ph_loop_bind_pass
   bool pass_bound = false;
@@ -4108,12 +4110,15 @@ bool pick_mid(int n, int m, int *blk, int *pc, int *pr) {
      // blocks' 128 (whose polish spilled 172 VGPRs at F3).  Measured at F3
      // iterations 30-34 (tools/mid_polish_prof.py): 14.3 ms per PH iteration
      // against 16.0 with <1024,2,1> (profiles/r03/mid_polish_f3_geom512.txt).
+     // Only past 1024 lines: with one line per thread the 1024-thread block
+     // is the faster one (sslp, n = 705: 23.9 against 25.4 ms per PH
+     // iteration, profiles/r06/sslp_geom_ab.txt).
      // PHGPU_MID_GEOM=1024 keeps the 1024-thread instances (measurement hook).
     static const int g = [] {
       const char *e = std::getenv("PHGPU_MID_GEOM");
       return e ? std::atoi(e) : 512;
     }();
-    if (g == 512 && mx > 512 && n <= 1536 && m <= 1536) {
+    if (g == 512 && mx > 1024 && n <= 1536 && m <= 1536) {
       *blk = 512;
       *pc = (n + 511) / 512;
       *pr = (m + 511) / 512;
@@ -4886,6 +4891,23 @@ static int mid_grid_cap() {
   return e ? std::max(0, std::atoi(e)) : 0;
 }
 
+// The accepted active sets of the mid-size / big polish (MidArgs::aset: a
+// warm start's classification is the scenario's last accepted set instead of
+// thresholds on the point; PHGPU_MID_ASET=0: measurement hook, thresholds).
+static int aset_init(ph_batch *b) {
+  b->md.aset = nullptr;
+  b->md.aset_ok = nullptr;
+  const char *e = std::getenv("PHGPU_MID_ASET");
+  if (e && std::atoi(e) == 0) return PH_OK;
+  int rc = 0;
+  if ((rc = dalloc(&b->d_aset, (size_t)b->S * (b->n + b->m))) || (rc = dalloc(&b->d_aset_ok, (size_t)b->S)))
+    return rc;
+  HIP_OK(hipMemsetAsync(b->d_aset_ok, 0, (size_t)b->S * sizeof(int32_t), b->stream));
+  b->md.aset = b->d_aset;
+  b->md.aset_ok = b->d_aset_ok;
+  return PH_OK;
+}
+
 // First-use setup of the big path (at bind: the scaling runs on its
 // workspace): occupancy, the resident grid, the workspace slices, the
 // phase work lists.
@@ -4910,10 +4932,6 @@ static int big_init(ph_batch *b) {
   if (const int cap = mid_grid_cap()) grid = std::min(grid, cap);
   b->big_grid = grid;
   b->bg.ws_blocks = grid;
-  {  // (PHGPU_BIG_QP_PDAS=1: a warm prox-QP polish classifies by the PDAS rule; A/B hook)
-    const char *e = std::getenv("PHGPU_BIG_QP_PDAS");
-    b->bg.qp_pdas = e && std::atoi(e) != 0 ? 1 : 0;
-  }
   int rc = 0;
   if ((rc = dalloc(&b->d_bws, (size_t)grid * b->bg.ws_stride)) ||
       (rc = dalloc(&b->d_vals_t, (size_t)b->S * b->nnz)) || (rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) ||
@@ -4943,6 +4961,7 @@ static int big_init(ph_batch *b) {
   }
   b->bg.ws_g = b->d_bws;
   b->bg.vals_t = b->d_vals_t;
+  if ((rc = aset_init(b))) return rc;
   b->mid_grid = b->mid_pgrid = grid;
   return PH_OK;
 }
@@ -4992,6 +5011,7 @@ static int mid_init(ph_batch *b) {
   }
   int rc = 0;
   if ((rc = dalloc(&b->d_mlist, (size_t)5 * b->S)) || (rc = dalloc(&b->d_mctr, 16))) return rc;
+  if ((rc = aset_init(b))) return rc;
   // the scenario-slowest copies of x, y and the PH terms (SolveArgs::xt)
   if ((rc = dalloc(&b->d_xt, (size_t)b->S * b->n)) || (b->m && (rc = dalloc(&b->d_yt, (size_t)b->S * b->m))) ||
       (b->K && (rc = dalloc(&b->d_pht, (size_t)b->S * 3 * b->K))))
@@ -6215,7 +6235,7 @@ void ph_batch_destroy(ph_batch_t b) {
                   b->d_eta, b->d_c, b->d_l, b->d_u, b->d_rl, b->d_ru, b->d_diag, b->d_summary,
                   b->d_cache, b->d_cache_ok, b->d_hint, b->d_hint_ok, b->d_wl, b->d_wl2, b->d_ctr,
                   b->d_ul, b->d_xpart, b->d_sb, b->d_part,
-                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ssym, b->d_ksdev, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_err, b->d_vals_t,
+                  b->d_ctl, b->d_sym, b->d_sym16, b->d_ssym, b->d_ksdev, b->d_ws, b->d_xt, b->d_yt, b->d_pht, b->d_mlist, b->d_mctr, b->d_aset, b->d_aset_ok, b->d_err, b->d_vals_t,
                   b->d_bws, b->d_lpart, b->d_lbar, b->d_fin, b->d_fpart, b->d_teambar, b->d_teampart,
                   b->d_r_pb, b->d_r_pos, b->d_r_len, b->d_c_pb, b->d_c_pos, b->d_c_len};
   for (void *p : ptrs)

@@ -41,9 +41,13 @@ ph.run_device_loop(0, W, -1.0, chunk=1)
 lib = b.lib
 lib.ph_debug_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
 lib.ph_debug_phase_times.restype = ctypes.c_int32
+lib.ph_debug_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+lib.ph_debug_prof.restype = ctypes.c_int32
+prof = np.zeros(64, dtype=np.int64)
 it = W
 for k in range(NIT):
     b.set_timing(True)
+    lib.ph_debug_prof(b.handle, 1, None)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ph.run_device_loop(it, it + 1, -1.0, chunk=1)
@@ -56,6 +60,12 @@ for k in range(NIT):
                                   ctr.ctypes.data_as(ctypes.c_void_p))
     n_t, as_ms, po_ms, pd_ms = b.read_timing()
     b.set_timing(False)
+    lib.ph_debug_prof(b.handle, 1, prof.ctypes.data_as(ctypes.c_void_p))
+    nst, nsc = max(int(prof[29]), 1), max(int(prof[30]), 1)
+    # solve_mid's block clocks (100 MHz ticks): [22] setup [23] steps [24] checks [31] end
+    prof_s = (f"mid PDHG: {nsc} scenario-phases, {nst} steps, us/step (block) steps "
+              f"{prof[23] / nst / 100:.2f} checks {prof[24] / nst / 100:.2f}; us/scenario-phase setup "
+              f"{prof[22] / nsc / 100:.1f} end {prof[31] / nsc / 100:.1f}")
     iters = b.iters.cpu().numpy()
     order = np.argsort(-iters)[:8]
     d = b.diagnostics()
@@ -63,4 +73,4 @@ for k in range(NIT):
     print(f"pass {it}: {dt:.1f} ms wall; phases [{ph_s}] ms; lists {ctr[:7].tolist()}; "
           f"PDHG steps mean {iters.mean():.1f} max {iters.max()} >100: {(iters > 100).sum()} "
           f">500: {(iters > 500).sum()}; top {[(int(s), int(iters[s])) for s in order]}; "
-          f"how {np.bincount(d[:, 4].astype(int), minlength=4).tolist()}", flush=True)
+          f"how {np.bincount(d[:, 4].astype(int), minlength=4).tolist()}; {prof_s}", flush=True)

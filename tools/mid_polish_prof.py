@@ -47,7 +47,7 @@ print(f"PDHG steps over the {NIT} passes: {steps} (last pass max {int(b.iters.ma
 print(f"iters {START}..{START+NIT}: mid_kernel {t[4]} launches {t[5]/max(t[4],1):.3f} ms avg, "
       f"mid_polish {t[6]} launches {t[7]/max(t[6],1):.3f} ms avg")
 print(f"polishes {out[9]} ({out[9]/NIT:.0f}/iter), rounds {out[10]}, refinement solves {out[11]}, "
-      f"accepted {out[12]}")
+      f"accepted {out[12]} (in the first round {out[0]})")
 print(f"per polish (block-us): setup {us(out[15] + out[27])/npol:.1f} (scatter {us(out[27])/npol:.1f}) "
       f"factor {us(out[13])/npol:.1f} solves {us(out[14])/npol:.1f} check {us(out[25])/npol:.1f} "
       f"PDAS {us(out[26])/npol:.1f}")

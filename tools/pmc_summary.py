@@ -55,11 +55,11 @@ WORKLOADS = {
                                    "mid_polish_kernel": "mid_polish_kernel<512, 3, 2>"},
                        "forbid": ["active_set_kernel"], "once_per_solve": []},
     "farmer1k_c1000": {"scenarios_per_rank": 1000, "crops_multiplier": 1000,
-                       "require": {"big_kernel": None, "big_polish_kernel": "big_polish_kernel"},
+                       "require": {"big_kernel": None, "big_polish_kernel": "big_polish_kernel<false>"},
                        "forbid": ["active_set_kernel", "mid_kernel"], "once_per_solve": []},
     "sslp10k": {"scenarios_per_rank": 10000, "crops_multiplier": None,
-                "require": {"mid_kernel": "mid_kernel<512, 2, 1>",
-                            "mid_polish_kernel": "mid_polish_kernel<512, 2, 1>"},
+                "require": {"mid_kernel": "mid_kernel<1024, 1, 1>",
+                            "mid_polish_kernel": "mid_polish_kernel<1024, 1, 1>"},
                 "forbid": ["active_set_kernel"], "once_per_solve": []},
 }
 
