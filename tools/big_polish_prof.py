@@ -27,7 +27,7 @@ lib = b.lib
 lib.ph_debug_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
 lib.ph_debug_prof.restype = ctypes.c_int32
 out = np.zeros(32, dtype=np.int64)
-names = {9: "polishes", 10: "rounds", 11: "refinement solves", 12: "accepted", 1: "nothing to change",
+names = {9: "polishes", 0: "accepted in the first round", 10: "rounds", 11: "refinement solves", 12: "accepted", 1: "nothing to change",
          2: "non-finite", 3: "round limit", 4: "refinement short", 6: "ep fails", 7: "ed fails",
          8: "eg fails", 20: "steps cut by the ratio test", 21: "full steps"}
 def report(tag):
