@@ -4944,6 +4944,16 @@ static int big_init(ph_batch *b) {
   b->big_tgrid = grid;
   b->bg.team_bar = b->bg.team_abort = nullptr;
   b->bg.team_part = nullptr;
+  {
+    // (F4, 12,000 columns: 8 blocks 38.0 ms per PH iteration, 16: 40.0, 64:
+    // 40.6, 4: 44.0; UC, 69,902 rows: 64 13.2 s, 16: 20.4 s --
+    // profiles/r06/f4_team_cap_ab.txt: about a line per thread, not fewer)
+    const int lines = std::max(b->n, b->m);
+    int cap = 2;
+    while (cap < BIG_TEAM_MAX && (long)2 * cap * BIG_BLOCK <= lines) cap *= 2;
+    if (const char *e = std::getenv("PHGPU_BIG_TEAM_CAP")) cap = std::max(2, std::min(BIG_TEAM_MAX, std::atoi(e)));
+    b->bg.team_cap = cap;
+  }
   const char *te = std::getenv("PHGPU_BIG_TEAMS");
   int per_cu_t = 0, coop = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, big_team_kernel, BIG_BLOCK, BIG_SMALL_LDS));
