@@ -38,6 +38,7 @@ namespace {
 
 thread_local std::string g_err;
 std::atomic<int> g_live_batches{0};  // batches alive in the process (coop_enabled)
+std::atomic<int> g_live_big{0};      // big-path batches among them (big_team_grid)
 
 int fail(int code, const std::string &msg) {
   g_err = msg;
@@ -4018,6 +4019,7 @@ struct ph_batch {
   int big_grid = 0;             // resident blocks of the big phase kernels
   int big_tgrid = 0;            // big_kernel's launch grid (teams: every resident block)
   int32_t *d_teambar = nullptr; // [big_tgrid + 1] team barrier counters, abort flag
+  bool big_counted = false;     // counted in g_live_big
   double *d_teampart = nullptr; // team reduction partials
   // persistent device loop (ph_loop_run, loop_kernel)
   int loop_grid = 0, loop_spw = 0, loop_G = 0;  // resident blocks, scenario slots per wave, for G
@@ -4409,13 +4411,19 @@ static int mid_setup(ph_batch *b, const int32_t *row_ptr, const int32_t *col_idx
   }
   std::vector<int32_t> rlong(b->m, 0), clong(b->n, 0), lr, lc;
   if (big) {
+    // (PHGPU_BIG_LONG: measurement hook for the line length past which a
+    // wave sums the line, BIG_LONG)
+    static const int long_at = [] {
+      const char *e = std::getenv("PHGPU_BIG_LONG");
+      return e ? std::max(4, std::atoi(e)) : BIG_LONG;
+    }();
     for (int i = 0; i < b->m; ++i)
-      if (row_ptr[i + 1] - row_ptr[i] > BIG_LONG) {
+      if (row_ptr[i + 1] - row_ptr[i] > long_at) {
         rlong[i] = 1;
         lr.push_back(i);
       }
     for (int j = 0; j < b->n; ++j)
-      if (col_ptr[j + 1] - col_ptr[j] > BIG_LONG) {
+      if (col_ptr[j + 1] - col_ptr[j] > long_at) {
         clong[j] = 1;
         lc.push_back(j);
       }
@@ -4972,6 +4980,10 @@ static int big_init(ph_batch *b) {
   b->bg.ws_g = b->d_bws;
   b->bg.vals_t = b->d_vals_t;
   if ((rc = aset_init(b))) return rc;
+  if (!b->big_counted) {
+    b->big_counted = true;
+    g_live_big.fetch_add(1);
+  }
   b->mid_grid = b->mid_pgrid = grid;
   return PH_OK;
 }
@@ -5047,6 +5059,18 @@ static long big_polish_max_contrib() {
   return e ? std::atol(e) : 16L << 20;
 }
 
+// The PDHG phase grid of a big batch: every resident block, or with several
+// big batches in the process (a hub and its spokes on their own streams) an
+// equal share of them, so that one cylinder's cooperative team launch does
+// not wait for the whole device -- i.e. for the other cylinder's phase
+// launch, which on UC runs up to a million PDHG steps -- to drain.
+static int big_team_grid(const ph_batch *b) {
+  int tg = b->big_tgrid;
+  const int nb = g_live_big.load();
+  if (nb > 1 && coop_enabled()) tg = std::max(8, (tg / nb) & ~7);
+  return tg;
+}
+
 static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
   a.polish = opts ? opts->polish : 1;
   if (b->big && !b->bg.sd_on && b->sym.ncontrib > big_polish_max_contrib()) a.polish = 0;
@@ -5110,10 +5134,10 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
       if (b->bg.team_bar)  // the teams' barrier counters and abort flag
         hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(WAVE), 0, b->stream, b->d_teambar, b->big_tgrid + 1);
       if (b->big_ylds)
-        hipLaunchKernelGGL(big_kernel<true>, dim3(b->big_tgrid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
+        hipLaunchKernelGGL(big_kernel<true>, dim3(big_team_grid(b)), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
                            a, b->bg, ph);
       else
-        hipLaunchKernelGGL(big_kernel<false>, dim3(b->big_tgrid), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
+        hipLaunchKernelGGL(big_kernel<false>, dim3(big_team_grid(b)), dim3(BIG_BLOCK), b->big_lds_bytes, b->stream,
                            a, b->bg, ph);
       HIP_OK(hipGetLastError());
       if (b->bg.team_bar) {  // (exits at once unless the phase's list is short)
@@ -5122,7 +5146,7 @@ static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
         MidPhase tp = ph;
         void *args[3] = {&ta, &tb, &tp};
         bool placed = true;
-        if (int rc = launch_coop((const void *)big_team_kernel, dim3(b->big_tgrid), dim3(BIG_BLOCK), args,
+        if (int rc = launch_coop((const void *)big_team_kernel, dim3(big_team_grid(b)), dim3(BIG_BLOCK), args,
                                  BIG_SMALL_LDS, b->stream, &placed))
           return rc;
         if (!placed)  // big_kernel already ran with teams on: the list would be left unsolved
@@ -6252,6 +6276,7 @@ void ph_batch_destroy(ph_batch_t b) {
     if (p) (void)hipFree(p);
   for (hipEvent_t e : b->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : b->pev) (void)hipEventDestroy(e);
+  if (b->big_counted) g_live_big.fetch_sub(1);
   delete b;
   g_live_batches.fetch_sub(1);
 }
