@@ -3009,6 +3009,7 @@ struct FinArgs {
   double *xbar, *xsqbar, *W, *absdiff, *hist;
   int has_md;
   unsigned long long *prof;  // phase stamps (ph_debug_prof slots 16-19, 29-31) or null
+  int tail_delay_us;  // debug (PHGPU_FIN_TAIL_DELAY_US): tail blocks start their wait this late
 };
 
 __device__ __forceinline__ int fin_load(const int32_t *p) {
@@ -3112,6 +3113,10 @@ __global__ void __launch_bounds__(WAVE) finish_kernel(SolveArgs a, MidArgs md, F
     if (lane == 0) fin_ticket(fin + FIN_DONE + 16 * (b & 7));
     if (f.prof && lane == 0) atomicMax(&f.prof[17], wall_clock64());
     if (b >= f.tb) return;
+    if (f.tail_delay_us > 0 && threadIdx.x == 0) {  // debug: a late tail block (fin_reset must wait for it)
+      const unsigned long long t0 = wall_clock64();
+      while (wall_clock64() - t0 < 100ull * (unsigned long long)f.tail_delay_us) __builtin_amdgcn_s_sleep(8);
+    }
     fin_wait(fin + FIN_DONE, f.np, 8, a.err);
     if (lane == 0) fin_ticket(fin + FIN_TPASS);  // (the resetting block waits for every tail block's)
     const int count = min(fin_load(a.wl2_count), S);
@@ -4255,6 +4260,13 @@ static int kkt_knobs(ph_batch *b) {
     if (e) {
       const int v = std::max(0, std::min(2, std::atoi(e)));
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_pin_rows), &v, sizeof(v)));
+    }
+  }
+  {  // PHGPU_MID_SOLVES0: solves of the mid-size polish round's first pass
+    const char *e = std::getenv("PHGPU_MID_SOLVES0");
+    if (e) {
+      const int v = std::max(1, std::min(KKT_REFINE, std::atoi(e)));
+      HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_first_solves), &v, sizeof(v)));
     }
   }
   {  // PHGPU_KKT_REFINE_TOL: the polish's refinement stopping tolerance
@@ -5995,6 +6007,10 @@ static int loop_pass_fused(ph_batch *b, bool first, bool u_next, size_t fin_lds,
   f.nsum = p.G * f.C;
   f.nu = u_next ? f.C : 0;
   f.has_md = has_md;
+  {  // (read per call, as PHGPU_FUSED: the test sets it for one batch)
+    const char *e = std::getenv("PHGPU_FIN_TAIL_DELAY_US");
+    f.tail_delay_us = e && *e ? std::max(0, std::min(100000, std::atoi(e))) : 0;
+  }
   const size_t need = 2 * (size_t)f.nsum + (size_t)f.C;
   if (!b->d_fin) {
     if (int rc = dalloc(&b->d_fin, FIN_WORDS)) return rc;

@@ -1356,6 +1356,25 @@ def test_fused_pass_matches_five_launch_chain(monkeypatch):
         assert _rel(a, b_) < 5e-8
 
 
+def test_finish_kernel_reset_waits_for_late_tail_blocks(monkeypatch):
+    """Advisor r5 (medium): the block that zeroes finish_kernel's counters
+    must not do so while a tail block still polls FIN_DONE (the tail list is
+    empty in most passes, so nothing else waits for the tail blocks).  The
+    tail blocks are held back 2 ms before their wait (debug hook
+    PHGPU_FIN_TAIL_DELAY_US), well past the pass's ~40 µs: the loop must run
+    without a barrier timeout and give the undelayed trajectory (to the
+    solves' tolerance: which block polishes a miss, and so the cache refresh
+    order, depends on timing; measured 2e-9)."""
+    base = {"PHGPU_PERSIST": "0", "PHGPU_PRIME": "0", "PHGPU_FUSED": "1"}
+    p = _farmer_loop(1000, 20, {**base, "PHGPU_FIN_TAIL_DELAY_US": "2000"}, monkeypatch)
+    q = _farmer_loop(1000, 20, {**base, "PHGPU_FIN_TAIL_DELAY_US": "0"}, monkeypatch)
+    assert p[7] and q[7], "the fused form did not run"
+    assert p[0] == q[0] == 20 and p[1] == q[1]
+    assert np.allclose(p[2], q[2], rtol=1e-8, atol=1e-12)
+    for a, b_ in zip(p[3:6], q[3:6]):
+        assert _rel(a, b_) < 5e-8
+
+
 def test_grouped_cached_maps_match_one_wave(monkeypatch):
     """active_set_g_kernel (four scenarios per wave, as_evalg) against
     active_set_kernel (one scenario per wave, as_eval) over 30 PH iterations
