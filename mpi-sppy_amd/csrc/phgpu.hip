@@ -4269,6 +4269,13 @@ static int kkt_knobs(ph_batch *b) {
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_first_solves), &v, sizeof(v)));
     }
   }
+  {  // PHGPU_REFINE_REL: the refinement tolerance's factor on the KKT tolerance
+    const char *e = std::getenv("PHGPU_REFINE_REL");
+    if (e) {
+      const double t = std::atof(e);
+      HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_refine_rel), &t, sizeof(t)));
+    }
+  }
   {  // PHGPU_KKT_REFINE_TOL: the polish's refinement stopping tolerance
     const char *e = std::getenv("PHGPU_KKT_REFINE_TOL");
     if (e) {

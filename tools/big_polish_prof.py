@@ -36,6 +36,10 @@ def report(tag):
     st = b.status.cpu().numpy()
     print(tag, {v: int(out[k]) for k, v in names.items()}, "how", np.bincount(d[:, 4].astype(int), minlength=4),
           "not optimal", int((st != 0).sum()), flush=True)
+    npol = max(int(out[9]), 1)
+    if out[13] or out[14]:  # the prox-QP polish's phase clocks (100 MHz ticks)
+        print("  block-us per polish: classification %.1f factor %.1f solves %.1f check %.1f "
+              "re-classification %.1f" % tuple(out[k] / npol / 100.0 for k in (17, 13, 14, 15, 16)), flush=True)
     if out[22]:  # the first gap-only failure's decomposition (polish_big debug slots 23..29)
         g = out[23:30].copy().view(np.float64)
         print("  gap-only failure: free cols %.3e fixed cols %.3e active rows %.3e inactive rows %.3e "
