@@ -39,6 +39,7 @@ namespace {
 thread_local std::string g_err;
 std::atomic<int> g_live_batches{0};  // batches alive in the process (coop_enabled)
 std::atomic<int> g_live_big{0};      // big-path batches among them (big_team_grid)
+std::atomic<int> g_own_stream{0};    // batches created on a stream of their own (spokes)
 
 int fail(int code, const std::string &msg) {
   g_err = msg;
@@ -4025,6 +4026,7 @@ struct ph_batch {
   int big_tgrid = 0;            // big_kernel's launch grid (teams: every resident block)
   int32_t *d_teambar = nullptr; // [big_tgrid + 1] team barrier counters, abort flag
   bool big_counted = false;     // counted in g_live_big
+  bool own_stream = false;      // created on a stream of its own (counted in g_own_stream)
   double *d_teampart = nullptr; // team reduction partials
   // persistent device loop (ph_loop_run, loop_kernel)
   int loop_grid = 0, loop_spw = 0, loop_G = 0;  // resident blocks, scenario slots per wave, for G
@@ -4673,6 +4675,10 @@ int ph_batch_create(ph_batch_t *out, int32_t S, int32_t n, int32_t m, int32_t nn
   }
   *out = b;
   g_live_batches.fetch_add(1);
+  if (stream) {
+    b->own_stream = true;
+    g_own_stream.fetch_add(1);
+  }
   return PH_OK;
 }
 
@@ -4878,7 +4884,11 @@ static int phase_event(ph_batch *b, int kind) {
 static bool coop_enabled() {
   const char *e = std::getenv("PHGPU_COOP");
   if (e && *e) return std::atoi(e) != 0;
-  return g_live_batches.load() > 1;
+  // (batches that can run at the same time: several, one of them on a stream
+  // of its own -- a spoke's; two batches on the default stream are ordered,
+  // and a cooperative launch costs ~10 ms per pass when another process
+  // shares the device, profiles/r06/mr2_coop_ab.txt)
+  return g_live_batches.load() > 1 && g_own_stream.load() > 0;
 }
 
 static int launch_coop(const void *f, dim3 grid, dim3 block, void **args, size_t lds, hipStream_t s,
@@ -6300,6 +6310,7 @@ void ph_batch_destroy(ph_batch_t b) {
   for (hipEvent_t e : b->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : b->pev) (void)hipEventDestroy(e);
   if (b->big_counted) g_live_big.fetch_sub(1);
+  if (b->own_stream) g_own_stream.fetch_sub(1);
   delete b;
   g_live_batches.fetch_sub(1);
 }
