@@ -860,8 +860,11 @@ class PHBase(SPBase):
             # several ranks on RCCL: the pass is a collective + one library
             # call, each a host round trip of ~10-20 us against ~50 us of GPU
             # work at F2, so the chunk is replayed as one graph with the
-            # collectives captured on the batch's stream
-            return coll and self.comm.size > 1
+            # collectives captured on the batch's stream -- for one-wave
+            # batches (n + m <= 63) only: mid-size and big chunks stay eager
+            # (their replay is the experimental path above, and their passes
+            # are milliseconds long, so the host's round trips do not show)
+            return coll and self.comm.size > 1 and b.n + b.m <= 63
         return bool(opt)
 
     def _capture_chunk(self, kw, chunk):
