@@ -740,7 +740,9 @@ def _parser():
     ap.add_argument("--hbm-steps", type=int, default=5)
     ap.add_argument("--graphs", type=int, default=0,
                     help="replay the timed device-loop chunk as a HIP graph (0: eager launches, "
-                         "one ph_loop_pass call per PH iteration)")
+                         "one ph_loop_pass call per PH iteration; -1: the library's 'auto', "
+                         "graphs with the RCCL collective captured on several ranks -- not the "
+                         "default: that capture has run on a one-rank RCCL group only)")
     ap.add_argument("--f4-scens", type=int, default=1000,
                     help="scenarios per rank of the F4 companion config (big path); 0 = skip")
     ap.add_argument("--f4-crops", type=int, default=1000)
@@ -756,6 +758,10 @@ def _parser():
                          "it (its timed window is then the last --hbm-steps solve calls of the "
                          "process, the window tools/pmc_summary.py reads); prints its JSON")
     return ap
+
+
+def _graphs_opt(args):
+    return "auto" if args.graphs < 0 else bool(args.graphs)
 
 
 def _cpu_baseline_from_args():
@@ -816,7 +822,7 @@ def run():
             "defaultPHrho": args.rho, "convthresh": -1.0, "verbose": False,
             "display_progress": False, "display_timing": False,
             "iter0_solver_options": {}, "iterk_solver_options": {},
-            "device_loop_graphs": bool(args.graphs)}
+            "device_loop_graphs": _graphs_opt(args)}
     _progress(f"building {S} scenarios (crops_multiplier {c})")
     ph = PH(opts, names, farmer.scenario_creator,
             scenario_creator_kwargs={"crops_multiplier": c})
@@ -869,7 +875,7 @@ def run():
     lk_n, lk_ms, lk_passes = b.loop_read_timing()
     sb_ = b.loop_status()
     b.set_timing(False)
-    ph.PHoptions["device_loop_graphs"] = bool(args.graphs)
+    ph.PHoptions["device_loop_graphs"] = _graphs_opt(args)
     nt = max(n_t, 1)
     as_ms, po_ms, pd_ms = as_ms / nt, po_ms / nt, pd_ms / nt
     mid = (nk + np_) > 0      # a mid-size batch (--crops >= 6): its phase kernels instead
