@@ -40,6 +40,7 @@ thread_local std::string g_err;
 std::atomic<int> g_live_batches{0};  // batches alive in the process (coop_enabled)
 std::atomic<int> g_live_big{0};      // big-path batches among them (big_team_grid)
 std::atomic<int> g_own_stream{0};    // batches created on a stream of their own (spokes)
+std::atomic<int> g_own_big{0};       // big-path batches among those
 
 int fail(int code, const std::string &msg) {
   g_err = msg;
@@ -5012,6 +5013,7 @@ static int big_init(ph_batch *b) {
   if (!b->big_counted) {
     b->big_counted = true;
     g_live_big.fetch_add(1);
+    if (b->own_stream) g_own_big.fetch_add(1);
   }
   b->mid_grid = b->mid_pgrid = grid;
   return PH_OK;
@@ -5093,21 +5095,24 @@ static long big_polish_max_contrib() {
 // equal share of them, so that one cylinder's cooperative team launch does
 // not wait for the whole device -- i.e. for the other cylinder's phase
 // launch, which on UC runs up to a million PDHG steps -- to drain.
+// (the batches that can run at once: the spokes' -- each on a stream of its
+// own -- and one on the default stream, a hub's; batches on the default
+// stream are ordered with each other, whatever their number)
 static int big_team_grid(const ph_batch *b) {
   int tg = b->big_tgrid;
-  const int nb = g_live_big.load();
+  const int nb = g_own_big.load() + 1;
   if (nb > 1 && coop_enabled()) tg = std::max(8, (tg / nb) & ~7);
   return tg;
 }
-// Every live batch is big and the PDHG grids are shared (big_team_grid):
-// the team kernels of all of them fit on the device at once (their other
-// kernels never wait on another block).  PHGPU_COOP=1 keeps the
-// cooperative launch (measurement hook).
+// Every spoke batch is big and the PDHG grids are shared (big_team_grid):
+// the team kernels of a big hub and its spokes fit on the device at once
+// (their other kernels never wait on another block), so they launch
+// plainly.  PHGPU_COOP=1 keeps the cooperative launch (measurement hook).
 static bool big_grids_shared() {
   const char *e = std::getenv("PHGPU_COOP");
   if (e && *e && std::atoi(e) == 1) return false;
-  const int nb = g_live_big.load();
-  return nb > 1 && nb == g_live_batches.load() && coop_enabled();
+  const int ns = g_own_stream.load();
+  return ns > 0 && g_own_big.load() == ns && coop_enabled();
 }
 
 static int mid_solve(ph_batch *b, SolveArgs &a, const ph_solve_opts *opts) {
@@ -6329,6 +6334,7 @@ void ph_batch_destroy(ph_batch_t b) {
   for (hipEvent_t e : b->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : b->pev) (void)hipEventDestroy(e);
   if (b->big_counted) g_live_big.fetch_sub(1);
+  if (b->big_counted && b->own_stream) g_own_big.fetch_sub(1);
   if (b->own_stream) g_own_stream.fetch_sub(1);
   delete b;
   g_live_batches.fetch_sub(1);
