@@ -1211,9 +1211,11 @@ def test_uc_lp_relaxation_matches_oracle():
     names = uc.all_scenario_names(3)
     opts = _opts(PHIterLimit=1, defaultPHrho=1.0, convthresh=-1.0)
     # PDHG only (the factorisation is past the big polish's size limit):
-    # Scenario1's LP takes ~612k steps, the prox-QPs ~170k
-    opts["iter0_solver_options"] = {"pdhg_max_iters": 1000000}
-    opts["iterk_solver_options"] = {"pdhg_max_iters": 400000}
+    # Scenario1's LP takes ~612k steps, the prox-QPs ~170k; the limits are
+    # twice what a solve may take (asserted below), so a pass is far from
+    # any step limit (the margin was 1M against ~850k)
+    opts["iter0_solver_options"] = {"pdhg_max_iters": 2000000}
+    opts["iterk_solver_options"] = {"pdhg_max_iters": 1000000}
     ph = PH(dict(opts), names, uc.scenario_creator, rho_setter=uc.scenario_rhos)
     ph.PH_Prep()
     ph.subproblem_creation()
@@ -1222,6 +1224,7 @@ def test_uc_lp_relaxation_matches_oracle():
     S, n, m = b.S, b.n, b.m
     assert (n, m) == (56869, 69902)
     assert np.all(b.status.cpu().numpy() == 0)
+    assert int(b.iters.max().item()) <= 1000000, int(b.iters.max().item())
     vals = np.array([gold["values"][nm] for nm in names])
     ob = b.dbound.cpu().numpy() + b.const.cpu().numpy()
     assert np.all(np.abs(ob - vals) <= 1e-7 * np.abs(vals)), (ob, vals)
@@ -1246,6 +1249,7 @@ def test_uc_lp_relaxation_matches_oracle():
         assert _rel(ph.W.view(ph.K, S).cpu().numpy().T, np.array(orc.W)) < 1e-12
         ph.solve_loop(solver_options=ph.current_solver_options)
         assert np.all(b.status.cpu().numpy() == 0), k
+        assert int(b.iters.max().item()) <= 500000, int(b.iters.max().item())
         X = b.x.view(n, S).cpu().numpy()
         Y = b.y.view(m, S).cpu().numpy()
         W = ph.W.view(ph.K, S).cpu().numpy()
